@@ -1,0 +1,89 @@
+"""ctypes binding of libsudoku_hip.so (C-ABI declared in include/sudoku_hip.h).
+
+The shared library is built in-tree (distributed_sudoku_solver_amd/libsudoku_hip.so,
+see csrc/Makefile or __graft_entry__.build()).  There is no fallback: if the
+library is missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SDK_LIB_PATH", os.path.join(HERE, "libsudoku_hip.so"))
+HEADER = os.path.join(os.path.dirname(HERE), "include", "sudoku_hip.h")
+
+SDK_OK = 0
+SDK_EINVAL = -1
+SDK_EHIP = -2
+SDK_ENOMEM = -3
+
+SDK_SOLVED = 1
+SDK_UNSOLVABLE = 0
+SDK_BUDGET_HIT = -2
+
+SDK_CHECK_OK = 1
+SDK_CHECK_RAW_NAMEERROR = 2
+
+SDK_OPT_ORDER = 1
+SDK_OPT_NODE_BUDGET = 2
+SDK_OPT_WAVES_PER_CU = 3
+
+SDK_ORDER_MRV_UNIQUE = 0
+SDK_ORDER_LEX = 1
+
+# every symbol the header declares: name -> (restype, argtypes)
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+SIGNATURES = {
+    "sdk_abi_version": (ctypes.c_int, []),
+    "sdk_last_error": (ctypes.c_char_p, []),
+    "sdk_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "sdk_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "sdk_destroy": (ctypes.c_int, [_vp]),
+    "sdk_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int64]),
+    "sdk_get_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
+    "sdk_check_batch": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
+    "sdk_solve_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz]),
+    "sdk_count_solutions": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_int8)]),
+    "sdk_dev_alloc": (ctypes.c_int, [_vp, _sz, ctypes.POINTER(_vp)]),
+    "sdk_dev_free": (ctypes.c_int, [_vp, _vp]),
+    "sdk_memcpy_h2d": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
+    "sdk_memcpy_d2h": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
+    "sdk_synchronize": (ctypes.c_int, [_vp]),
+    "sdk_check_batch_dev": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
+    "sdk_solve_batch_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz]),
+    "sdk_timer_reset": (ctypes.c_int, [_vp]),
+    "sdk_timer_read": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+}
+
+_lib = None
+
+
+class SudokuHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libsudoku_hip.so (once). Raises if it is missing: no CPU fallback exists."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SudokuHipError(
+            f"{LIB_PATH} not found: build it with `make -C distributed_sudoku_solver_amd/csrc` "
+            "or `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != SDK_OK:
+        msg = load().sdk_last_error()
+        msg = msg.decode() if msg else ""
+        raise SudokuHipError(f"{what} failed ({rc}): {msg}")
+    return rc

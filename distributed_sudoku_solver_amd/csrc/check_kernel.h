@@ -1,0 +1,131 @@
+// check_kernel.h -- batched Sudoku.check() (sudoku.py:43-94) as an HBM-streaming kernel.
+//
+// Layout: boards uint8[n][81] contiguous in HBM, verdict uint8[n].
+// Algorithmic traffic: 81 B read + 1 B written per board.
+//
+// One 256-thread workgroup owns a tile of 256 boards = 20,736 B = 1,296 x 16 B.
+// The tile is streamed HBM -> LDS with coalesced dwordx4 loads (every lane reads
+// 16 B, a wave reads 1 KiB contiguous), then each thread validates one board from
+// LDS: 22 ds_read_b32 + v_alignbyte re-align the 81-B record (81i mod 4 = i mod 4)
+// into 21 dwords, so no unaligned global access and no byte-granular HBM reads.
+//
+// Per unit the reference rule is literal: `sum == 45 and len(set) == 9`.
+//  * fast path (every byte of the board <= 9): acc_u = sum 2^v over the unit.
+//    For 9 values in 0..9:  literal rule <=> multiset {1..9} <=> acc_u == 0x3FE
+//    (merging equal powers of two reduces the term count, and 0x3FE has 9 bits).
+//  * exact path (some byte >= 10, any uint8):  x = (v << 22) + 2^min(v,18);
+//    pass <=> popc(acc & 0x3FFFFF) == 9 and (acc >> 22) == 45.  9 distinct
+//    non-negative values summing to 45 are all <= 17, so clamping at 18 never
+//    merges two passing values; with popc == 9 at most one value is >= 18, the
+//    sum is then <= 363 and the 10-bit field cannot wrap.
+// The raw-NameError bit needs the exact box(0,0) sum (sudoku.py:68 evaluates
+// the sum before the broken set expression), accumulated separately.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdk {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCheckThreads = 256;
+constexpr int kCheckTileBytes = kCheckThreads * 81;          // 20736
+constexpr int kCheckTileVec = kCheckTileBytes / 16;          // 1296 x uint4
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[21], int k) {
+    return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+}
+
+__device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int t) {
+    const int start = 81 * t;
+    const int d0 = start >> 2;
+    const uint32_t sh = (uint32_t)(start & 3);
+    uint32_t raw[22];
+#pragma unroll
+    for (int k = 0; k < 22; ++k) raw[k] = tile_dw[d0 + k];
+    uint32_t w[21];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) w[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh);
+    w[20] &= 0xFFu;  // only cell 80 belongs to this board
+
+    // any byte >= 10 ?  ((b & 0x7F) + 0x76) sets bit 7 iff (b & 0x7F) >= 10, no carry out of the byte
+    uint32_t big = 0;
+#pragma unroll
+    for (int k = 0; k < 21; ++k) big |= (((w[k] & 0x7F7F7F7Fu) + 0x76767676u) | w[k]) & 0x80808080u;
+
+    uint32_t rowacc[9], colacc[9], boxacc[9];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) rowacc[u] = colacc[u] = boxacc[u] = 0;
+    uint32_t box00 = 0;
+    uint8_t verdict;
+    if (big == 0) {
+#pragma unroll
+        for (int k = 0; k < 81; ++k) {
+            const int r = k / 9, c = k % 9, b = (r / 3) * 3 + c / 3;
+            const uint32_t v = byte_of(w, k);
+            const uint32_t p = 1u << v;
+            rowacc[r] += p; colacc[c] += p; boxacc[b] += p;
+            if (b == 0) box00 += v;
+        }
+        bool rows = true, cols = true, boxes = true;
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+            rows &= rowacc[u] == 0x3FEu;
+            cols &= colacc[u] == 0x3FEu;
+            boxes &= boxacc[u] == 0x3FEu;
+        }
+        verdict = (uint8_t)((rows && cols && boxes) ? 1u : 0u);
+        if (rows && cols && box00 == 45u) verdict |= 2u;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 81; ++k) {
+            const int r = k / 9, c = k % 9, b = (r / 3) * 3 + c / 3;
+            const uint32_t v = byte_of(w, k);
+            const uint32_t x = (v << 22) + (1u << min(v, 18u));
+            rowacc[r] += x; colacc[c] += x; boxacc[b] += x;
+            if (b == 0) box00 += v;
+        }
+        auto ok = [](uint32_t a) { return __popc(a & 0x3FFFFFu) == 9 && (a >> 22) == 45u; };
+        bool rows = true, cols = true, boxes = true;
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+            rows &= ok(rowacc[u]);
+            cols &= ok(colacc[u]);
+            boxes &= ok(boxacc[u]);
+        }
+        verdict = (uint8_t)((rows && cols && boxes) ? 1u : 0u);
+        if (rows && cols && box00 == 45u) verdict |= 2u;
+    }
+    return verdict;
+}
+
+__global__ __launch_bounds__(kCheckThreads) void check_kernel(const uint8_t* __restrict__ boards,
+                                                              uint8_t* __restrict__ verdict, uint64_t n) {
+    // +16 B: the last thread's 22nd dword read runs one dword past the tile.
+    __shared__ __attribute__((aligned(16))) u32x4 tile[kCheckTileVec + 1];
+    const int t = threadIdx.x;
+    const uint64_t ntiles = (n + kCheckThreads - 1) / kCheckThreads;
+    for (uint64_t tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
+        const uint64_t base = tix * kCheckThreads;
+        const uint64_t cnt = min((uint64_t)kCheckThreads, n - base);
+        const uint8_t* src = boards + base * 81;
+        if (cnt == (uint64_t)kCheckThreads) {
+            const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+#pragma unroll
+            for (int j = 0; j < kCheckTileVec / kCheckThreads; ++j)  // 5 full sweeps
+                tile[j * kCheckThreads + t] = __builtin_nontemporal_load(&s4[j * kCheckThreads + t]);
+            if (t < kCheckTileVec % kCheckThreads)                    // 16 remaining vectors
+                tile[(kCheckTileVec / kCheckThreads) * kCheckThreads + t] =
+                    __builtin_nontemporal_load(&s4[(kCheckTileVec / kCheckThreads) * kCheckThreads + t]);
+        } else {
+            uint8_t* tb = reinterpret_cast<uint8_t*>(tile);
+            for (uint64_t j = t; j < cnt * 81; j += kCheckThreads) tb[j] = src[j];
+        }
+        __syncthreads();
+        if ((uint64_t)t < cnt)
+            verdict[base + t] = check_board_lds(reinterpret_cast<const uint32_t*>(tile), t);
+        __syncthreads();
+    }
+}
+
+}  // namespace sdk

@@ -1,0 +1,324 @@
+// solve_kernel.h -- the solve path of DHTNode.solve_sudoku (DHT_Node.py:474-538) on gfx950.
+//
+// One board per wavefront (one 64-lane workgroup).  Lane l owns cell l (the "A"
+// half of its state word) and, for l < 17, cell 64+l (the "B" half).  A cell
+// state is 16 bits: bits 0..8 candidate digits 1..9, CLUE = given 1..9,
+// INERT = given 10..255 (the reference compares cells with `== guess` only, so
+// such a value never conflicts: utils.py:36,44,53).
+//
+// Constraint (exactly the naive DFS's): every pair of cells in a unit where at
+// least one cell is NOT a given must differ.  Given-vs-given duplicates are
+// ignored (the reference never validates clues).
+//
+// Propagation round (all in LDS, no atomics):
+//   1. every lane writes its cell states to s_cell[81];
+//   2. lanes 0..26 each summarise one unit (row/col/box) from its 9 cells:
+//        T     = digits of single-candidate cells (givens and solved),
+//        once  = digits with exactly one candidate cell (hidden singles) -- only
+//                in "exact" units (no INERT cell, no duplicate given), where
+//                every digit must occur exactly once in every completion,
+//        conflict = two non-given singles share a digit, a non-given single
+//                repeats a given, or an exact unit lost a digit entirely;
+//   3. every lane ORs its three unit summaries and updates its cells:
+//        cand &= ~T (naked-single elimination); cand & once -> hidden single.
+//   Repeated to a fixpoint; wave votes (__any/__ballot) decide CONTRA / SOLVED / OPEN.
+// Every step only removes digits that appear in no completion, so the set of
+// completions below a node is unchanged by propagation.
+//
+// Search.  Branch cell chosen with __ballot + ctz:
+//   ORDER_LEX: the lowest-index open cell, digits ascending.  All cells before
+//     it are forced, so the first completion found is the lexicographically
+//     first one = the reference's row-major ascending DFS result.
+//   ORDER_MRV: fewest candidates (ties: lowest index).  Used to count up to 2
+//     completions; a unique completion IS the lexicographically first one.  If
+//     2 are found the board is re-searched with ORDER_LEX.
+// The DFS stack (one 256-B snapshot of the wave's state words per level) lives
+// in a per-workgroup HBM region (L2-resident in practice); branch records (cell,
+// untried digits) live in LDS.
+//
+// Boards are handed out to persistent wavefronts CHUNK at a time by one atomic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdk {
+
+constexpr uint32_t kCands = 0x1FFu;
+constexpr uint32_t kClue = 0x200u;
+constexpr uint32_t kInert = 0x400u;
+constexpr uint32_t kFixed = kClue | kInert;
+constexpr int kMaxDepth = 81;
+constexpr uint32_t kChunk = 4;
+constexpr int kStackWordsPerBlock = kMaxDepth * 64;
+
+enum { P_CONTRA = 0, P_SOLVED = 1, P_OPEN = 2 };
+enum { ORDER_MRV = 0, ORDER_LEX = 1 };
+
+struct SolveArgs {
+    const uint8_t* in;
+    const uint16_t* mask;      // nullable: first-cell digit mask, bit d = digit d
+    uint8_t* out;
+    int8_t* status;
+    uint64_t* work;            // nullable
+    uint64_t n;
+    uint32_t* next;            // work counter (zeroed before launch)
+    uint32_t* stack;           // gridDim.x * kStackWordsPerBlock words
+    uint64_t budget;           // nodes per board, 0 = unlimited
+    int order;                 // SDK_ORDER_*
+    uint64_t limit;            // count mode only
+    unsigned long long* count; // count mode only
+    int count_mode;
+};
+
+__device__ __forceinline__ uint32_t cell_init(uint32_t v) {
+    return v == 0 ? kCands : (v <= 9 ? ((1u << (v - 1)) | kClue) : kInert);
+}
+
+__device__ __forceinline__ bool is_single(uint32_t v) { return v != 0 && (v & (v - 1)) == 0; }
+
+// candidates count of a branchable cell, else 0
+__device__ __forceinline__ uint32_t open_count(uint32_t x) {
+    return (x & kFixed) ? 0u : (uint32_t)__popc(x & kCands);
+}
+
+struct Wave {
+    uint32_t* s_cell;   // [96]
+    uint32_t* s_unit;   // [32]
+    uint32_t* s_br;     // [kMaxDepth]
+    uint32_t* stk;      // this workgroup's HBM stack
+    int lane;
+    bool hasB;
+    int uA0, uA1, uA2, uB0, uB1, uB2;
+    int ucell[9];
+};
+
+__device__ __forceinline__ void update_cell(uint32_t& x, uint32_t u, bool& bad, bool& chg) {
+    if (x & kFixed) return;
+    const uint32_t v = x & kCands;
+    if (v & (v - 1)) {
+        uint32_t v1 = v & ~u;
+        const uint32_t h = v1 & (u >> 16) & kCands;
+        if (h) {
+            if (h & (h - 1)) bad = true;
+            v1 = h;
+        }
+        if (v1 == 0) bad = true;
+        if (v1 != v) { chg = true; x = v1; }
+    } else if (v == 0) {
+        bad = true;
+    }
+}
+
+__device__ __forceinline__ int propagate(const Wave& w, uint32_t& sa, uint32_t& sb) {
+    for (;;) {
+        w.s_cell[w.lane] = sa;
+        if (w.hasB) w.s_cell[64 + w.lane] = sb;
+        __syncthreads();
+        uint32_t summ = 0;
+        if (w.lane < 27) {
+            uint32_t ones = 0, twos = 0, tn1 = 0, tn2 = 0, tc1 = 0, tc2 = 0, t = 0, inert = 0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const uint32_t x = w.s_cell[w.ucell[k]];
+                const uint32_t v = x & kCands;
+                const uint32_t sv = is_single(v) ? v : 0u;
+                t |= sv;
+                twos |= ones & v;
+                ones |= v;
+                const bool clue = (x & kClue) != 0;
+                const uint32_t cv = clue ? v : 0u;
+                tc2 |= tc1 & cv;
+                tc1 |= cv;
+                const uint32_t nv = clue ? 0u : sv;
+                tn2 |= tn1 & nv;
+                tn1 |= nv;
+                inert |= x & kInert;
+            }
+            bool conflict = (tn2 | (tn1 & tc1)) != 0;
+            uint32_t once = 0;
+            if (!inert && !tc2) {
+                if (ones != kCands) conflict = true;
+                once = ones & ~twos;
+            }
+            summ = t | (once << 16) | (conflict ? 0x80000000u : 0u);
+            w.s_unit[w.lane] = summ;
+        }
+        if (__any((int)(summ >> 31))) return P_CONTRA;
+        __syncthreads();
+        const uint32_t ua = w.s_unit[w.uA0] | w.s_unit[w.uA1] | w.s_unit[w.uA2];
+        const uint32_t ub = w.hasB ? (w.s_unit[w.uB0] | w.s_unit[w.uB1] | w.s_unit[w.uB2]) : 0u;
+        bool bad = false, chg = false;
+        update_cell(sa, ua, bad, chg);
+        if (w.hasB) update_cell(sb, ub, bad, chg);
+        if (__any((int)bad)) return P_CONTRA;
+        if (!__any((int)chg)) {
+            const bool open = open_count(sa) >= 2 || (w.hasB && open_count(sb) >= 2);
+            return __any((int)open) ? P_OPEN : P_SOLVED;
+        }
+    }
+}
+
+__device__ __forceinline__ void write_board(const Wave& w, uint8_t* dst, uint32_t inA, uint32_t inB,
+                                            uint32_t sa, uint32_t sb, bool solved) {
+    uint32_t a = inA, b = inB;
+    if (solved) {
+        if (a == 0) a = (uint32_t)__ffs(sa & kCands);
+        if (b == 0) b = (uint32_t)__ffs(sb & kCands);
+    }
+    dst[w.lane] = (uint8_t)a;
+    if (w.hasB) dst[64 + w.lane] = (uint8_t)b;
+}
+
+__device__ __forceinline__ void set_cell(const Wave& w, uint32_t& sa, uint32_t& sb, int cell, uint32_t d) {
+    if (cell < 64) {
+        if (w.lane == cell) sa = d;
+    } else {
+        if (w.lane == cell - 64) sb = d;
+    }
+}
+
+// Returns the number of completions found (stopping at `limit`, 0 = no limit),
+// or -1 when the node budget ran out.  The first completion is written to
+// `sol` when non-null.
+__device__ int64_t search(const Wave& w, int order, uint32_t sa0, uint32_t sb0, uint64_t limit,
+                          uint64_t budget, uint64_t& nodes, uint8_t* sol, uint32_t inA, uint32_t inB) {
+    uint32_t sa = sa0, sb = sb0;
+    int depth = 0;
+    int64_t count = 0;
+    for (;;) {
+        int r = propagate(w, sa, sb);
+        ++nodes;
+        if (budget && nodes > budget) return -1;
+        if (r == P_SOLVED) {
+            ++count;
+            if (count == 1 && sol) write_board(w, sol, inA, inB, sa, sb, true);
+            if (limit && (uint64_t)count >= limit) return count;
+            r = P_CONTRA;
+        }
+        if (r == P_OPEN) {
+            const uint32_t pa = open_count(sa);
+            const uint32_t pb = w.hasB ? open_count(sb) : 0u;
+            unsigned long long ma, mb;
+            if (order == ORDER_LEX) {
+                ma = __ballot(pa >= 2);
+                mb = __ballot(pb >= 2);
+            } else {
+                ma = mb = 0;
+                for (uint32_t k = 2; k <= 9; ++k) {
+                    ma = __ballot(pa == k);
+                    mb = __ballot(pb == k);
+                    if (ma | mb) break;
+                }
+            }
+            const int cell = ma ? (int)__builtin_ctzll(ma) : 64 + (int)__builtin_ctzll(mb);
+            const uint32_t src = cell < 64 ? sa : sb;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)src, cell & 63) & kCands;
+            const uint32_t d = m & (0u - m);
+            w.stk[depth * 64 + w.lane] = sa | (sb << 16);
+            if (w.lane == 0) w.s_br[depth] = (uint32_t)cell | ((m ^ d) << 16);
+            ++depth;
+            set_cell(w, sa, sb, cell, d);
+            continue;
+        }
+        // contradiction: resume the deepest level that still has untried digits
+        if (depth == 0) return count;
+        const uint32_t br = w.s_br[depth - 1];
+        const int cell = (int)(br & 0xFFu);
+        uint32_t rest = br >> 16;
+        const uint32_t d = rest & (0u - rest);
+        rest ^= d;
+        const uint32_t snap = w.stk[(depth - 1) * 64 + w.lane];
+        sa = snap & 0xFFFFu;
+        sb = snap >> 16;
+        if (rest == 0) {
+            --depth;
+        } else if (w.lane == 0) {
+            w.s_br[depth - 1] = (uint32_t)cell | (rest << 16);
+        }
+        set_cell(w, sa, sb, cell, d);
+    }
+}
+
+__global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
+    __shared__ uint32_t s_cell[96];
+    __shared__ uint32_t s_unit[32];
+    __shared__ uint32_t s_br[kMaxDepth];
+    Wave w;
+    w.s_cell = s_cell;
+    w.s_unit = s_unit;
+    w.s_br = s_br;
+    w.stk = a.stack + (size_t)blockIdx.x * kStackWordsPerBlock;
+    const int lane = threadIdx.x;
+    w.lane = lane;
+    w.hasB = lane < 17;
+    {
+        const int c = lane;
+        w.uA0 = c / 9;
+        w.uA1 = 9 + c % 9;
+        w.uA2 = 18 + (c / 27) * 3 + (c % 9) / 3;
+        const int cb = w.hasB ? 64 + lane : 0;
+        w.uB0 = cb / 9;
+        w.uB1 = 9 + cb % 9;
+        w.uB2 = 18 + (cb / 27) * 3 + (cb % 9) / 3;
+        const int u = lane < 27 ? lane : 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            int cell;
+            if (u < 9) cell = 9 * u + k;
+            else if (u < 18) cell = 9 * k + (u - 9);
+            else {
+                const int b = u - 18;
+                cell = ((b / 3) * 3 + k / 3) * 9 + (b % 3) * 3 + k % 3;
+            }
+            w.ucell[k] = cell;
+        }
+    }
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(a.next, kChunk);
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        if ((uint64_t)base >= a.n) break;
+        const uint64_t end = min((uint64_t)base + kChunk, a.n);
+        for (uint64_t i = base; i < end; ++i) {
+            const uint8_t* src = a.in + i * 81;
+            const uint32_t inA = src[lane];
+            const uint32_t inB = w.hasB ? (uint32_t)src[64 + lane] : 0u;
+            uint32_t sa = cell_init(inA);
+            uint32_t sb = w.hasB ? cell_init(inB) : kInert;
+            // TASK `range` restricts the lowest-index empty input cell only (DHT_Node.py:474,522,531)
+            const uint32_t fm = a.mask ? (((uint32_t)a.mask[i] >> 1) & kCands) : kCands;
+            const unsigned long long za = __ballot(inA == 0);
+            const unsigned long long zb = __ballot(w.hasB && inB == 0);
+            if (za) {
+                if (lane == (int)__builtin_ctzll(za)) sa &= fm | ~kCands;
+            } else if (zb) {
+                if (lane == (int)__builtin_ctzll(zb)) sb &= fm | ~kCands;
+            }
+            uint8_t* dst = a.out + i * 81;
+            uint64_t nodes = 0;
+            int8_t st;
+            if (a.count_mode) {
+                const int64_t c = search(w, ORDER_MRV, sa, sb, a.limit, a.budget, nodes, dst, inA, inB);
+                if (lane == 0) *a.count = (unsigned long long)(c < 0 ? 0 : c);
+                st = c < 0 ? (int8_t)-2 : (c > 0 ? (int8_t)1 : (int8_t)0);
+                if (c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
+            } else {
+                int64_t c;
+                if (a.order == ORDER_LEX) {
+                    c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, dst, inA, inB);
+                } else {
+                    c = search(w, ORDER_MRV, sa, sb, 2, a.budget, nodes, dst, inA, inB);
+                    if (c >= 2) c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, dst, inA, inB);
+                }
+                st = c < 0 ? (int8_t)-2 : (c > 0 ? (int8_t)1 : (int8_t)0);
+                if (c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
+            }
+            if (lane == 0) {
+                a.status[i] = st;
+                if (a.work) a.work[i] = nodes;
+            }
+        }
+    }
+}
+
+}  // namespace sdk

@@ -1,0 +1,207 @@
+"""SudokuEngine: numpy-level batch API over libsudoku_hip.so.
+
+This is the host side of the drop-in boundary.  Every method
+ends in a HIP kernel launched by the C library; nothing here computes a
+solution or a verdict.
+"""
+import ctypes
+import numbers
+
+import numpy as np
+
+from . import _lib as L
+
+ALL_DIGITS_MASK = 0x3FE  # bits 1..9: range(1, 10)
+INERT_VALUE = 10         # any given that is never equal to a digit 1..9
+
+
+# ----------------------------------------------------------------- encoding
+def _as_int(v):
+    """The reference compares cells with `==` (utils.py:22,36,44,53): 5.0 == 5, True == 1."""
+    if isinstance(v, numbers.Integral):
+        return int(v)
+    if isinstance(v, numbers.Real) and float(v).is_integer():
+        return int(v)
+    return None
+
+
+def encode_solve_grid(grid):
+    """9x9 (or flat 81) Python grid -> uint8[81] for the solver.
+
+    0 -> empty; a value equal to a digit 1..9 -> that digit; anything else is a
+    given that never equals a guess 1..9 (the reference never rejects it) and
+    is encoded as the inert value 10."""
+    flat = [v for row in grid for v in row] if len(grid) == 9 else list(grid)
+    if len(flat) != 81:
+        raise ValueError("a Sudoku grid has 81 cells")
+    out = np.empty(81, dtype=np.uint8)
+    for i, v in enumerate(flat):
+        iv = _as_int(v)
+        if iv == 0:
+            out[i] = 0
+        elif iv is not None and 1 <= iv <= 9:
+            out[i] = iv
+        else:
+            out[i] = INERT_VALUE
+    return out
+
+
+def encode_check_grid(grid):
+    """9x9 grid -> uint8[81] for the checker (literal sum/set rule needs exact values)."""
+    flat = [v for row in grid for v in row] if len(grid) == 9 else list(grid)
+    if len(flat) != 81:
+        raise ValueError("a Sudoku grid has 81 cells")
+    out = np.empty(81, dtype=np.uint8)
+    for i, v in enumerate(flat):
+        iv = _as_int(v)
+        if iv is None or not 0 <= iv <= 255:
+            raise ValueError(f"cell {i} = {v!r}: the HIP checker takes integers 0..255")
+        out[i] = iv
+    return out
+
+
+def range_to_mask(arr):
+    """TASK digit range (a `range` from split_array_in_middle, utils.py:1-9) -> first-cell mask.
+
+    bit d = digit d may be guessed at the lowest empty cell.  Guess 0 is never
+    valid in the reference (the empty cell itself holds 0, utils.py:36), so it
+    is dropped.  Order matters to the reference (`for guess in arr`), so only
+    ascending digit sequences in 0..9 are representable."""
+    vals = [_as_int(v) for v in arr]
+    if any(v is None or v < 0 or v > 9 for v in vals):
+        raise ValueError(f"digit range {arr!r} has values outside 0..9")
+    if any(b <= a for a, b in zip(vals, vals[1:])):
+        raise ValueError(f"digit range {arr!r} is not strictly ascending")
+    m = 0
+    for v in vals:
+        if v >= 1:
+            m |= 1 << v
+    return m
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+# ------------------------------------------------------------------- device
+class DeviceBuffer:
+    """A device allocation owned by an engine context (for resident-input benchmarks)."""
+
+    def __init__(self, engine, nbytes):
+        self.engine = engine
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        L.check(engine.lib.sdk_dev_alloc(engine.ctx, self.nbytes, ctypes.byref(p)), "sdk_dev_alloc")
+        self.ptr = p
+
+    def upload(self, host):
+        host = np.ascontiguousarray(host)
+        assert host.nbytes <= self.nbytes
+        L.check(self.engine.lib.sdk_memcpy_h2d(self.engine.ctx, self.ptr, _ptr(host), host.nbytes), "h2d")
+
+    def download(self, host):
+        assert host.flags.c_contiguous and host.nbytes <= self.nbytes
+        L.check(self.engine.lib.sdk_memcpy_d2h(self.engine.ctx, _ptr(host), self.ptr, host.nbytes), "d2h")
+        return host
+
+    def free(self):
+        if self.ptr is not None and self.engine.ctx is not None:
+            L.check(self.engine.lib.sdk_dev_free(self.engine.ctx, self.ptr), "sdk_dev_free")
+        self.ptr = None
+
+
+class SudokuEngine:
+    """One HIP device + stream.  Thread-safe (the C library serialises per context)."""
+
+    def __init__(self, device=0, order=None, node_budget=None, waves_per_cu=None):
+        self.lib = L.load()
+        ctx = ctypes.c_void_p()
+        L.check(self.lib.sdk_create(int(device), ctypes.byref(ctx)), f"sdk_create(device={device})")
+        self.ctx = ctx
+        self.device = device
+        if order is not None:
+            self.set_option(L.SDK_OPT_ORDER, order)
+        if node_budget is not None:
+            self.set_option(L.SDK_OPT_NODE_BUDGET, node_budget)
+        if waves_per_cu is not None:
+            self.set_option(L.SDK_OPT_WAVES_PER_CU, waves_per_cu)
+
+    # -------------------------------------------------------------- plumbing
+    def close(self):
+        if getattr(self, "ctx", None) is not None:
+            self.lib.sdk_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_option(self, key, value):
+        L.check(self.lib.sdk_set_option(self.ctx, key, int(value)), "sdk_set_option")
+
+    def get_option(self, key):
+        v = ctypes.c_int64()
+        L.check(self.lib.sdk_get_option(self.ctx, key, ctypes.byref(v)), "sdk_get_option")
+        return v.value
+
+    def synchronize(self):
+        L.check(self.lib.sdk_synchronize(self.ctx), "sdk_synchronize")
+
+    def timer_reset(self):
+        L.check(self.lib.sdk_timer_reset(self.ctx), "sdk_timer_reset")
+
+    def timer_read(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        L.check(self.lib.sdk_timer_read(self.ctx, ctypes.byref(ms), ctypes.byref(n)), "sdk_timer_read")
+        return ms.value, n.value
+
+    def alloc(self, nbytes):
+        return DeviceBuffer(self, nbytes)
+
+    # ----------------------------------------------------------- host batch
+    def check_batch(self, boards):
+        """uint8[n,81] -> uint8[n] verdict bits (SDK_CHECK_OK | SDK_CHECK_RAW_NAMEERROR)."""
+        boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
+        n = boards.shape[0]
+        verdict = np.empty(n, dtype=np.uint8)
+        L.check(self.lib.sdk_check_batch(self.ctx, _ptr(boards), _ptr(verdict), n), "sdk_check_batch")
+        return verdict
+
+    def solve_batch(self, boards, masks=None, want_work=False):
+        """uint8[n,81] (+ optional uint16[n] first-cell masks) -> (out uint8[n,81], status int8[n], work)."""
+        boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
+        n = boards.shape[0]
+        if masks is not None:
+            masks = np.ascontiguousarray(masks, dtype=np.uint16).reshape(n)
+        out = np.empty_like(boards)
+        status = np.empty(n, dtype=np.int8)
+        work = np.empty(n, dtype=np.uint64) if want_work else None
+        L.check(self.lib.sdk_solve_batch(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status),
+                                         _ptr(work), n), "sdk_solve_batch")
+        return out, status, work
+
+    def count_solutions(self, board, limit=0):
+        board = np.ascontiguousarray(board, dtype=np.uint8).reshape(81)
+        cnt = ctypes.c_uint64()
+        st = ctypes.c_int8()
+        L.check(self.lib.sdk_count_solutions(self.ctx, _ptr(board), int(limit), ctypes.byref(cnt), ctypes.byref(st)),
+                "sdk_count_solutions")
+        return cnt.value, st.value
+
+    # --------------------------------------------------------- device batch
+    def check_batch_dev(self, d_boards, d_verdict, n):
+        L.check(self.lib.sdk_check_batch_dev(self.ctx, d_boards.ptr, d_verdict.ptr, int(n)), "sdk_check_batch_dev")
+
+    def solve_batch_dev(self, d_in, d_out, d_status, n, d_mask=None, d_work=None):
+        L.check(self.lib.sdk_solve_batch_dev(self.ctx, d_in.ptr, d_mask.ptr if d_mask else None, d_out.ptr,
+                                             d_status.ptr, d_work.ptr if d_work else None, int(n)),
+                "sdk_solve_batch_dev")

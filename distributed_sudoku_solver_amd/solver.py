@@ -1,0 +1,113 @@
+"""Drop-in for the reference solve path: DHTNode.solve_sudoku (DHT_Node.py:474-538) and
+its main.py twin (main.py:301-354).
+
+Call contract kept from the reference:
+  * `puzzle` is a list of 9 lists of 9 numbers and is mutated in place:
+    completed (lexicographically first completion = the reference's row-major,
+    ascending-digit DFS result) when True is returned, untouched when False;
+  * `arr` (a TASK digit `range`) restricts only the lowest-index empty cell;
+  * returns a bool.
+The search itself runs in libsudoku_hip.so; this module only converts the grid.
+
+Node protocol side effects of the reference's recursive solver are applied once,
+before the (micro-second) device call instead of once per recursion level:
+cancellation (`task == []`, DHT_Node.py:481), one non-blocking UDP poll
+(DHT_Node.py:485-488), and the hand-off of half the digit range to a free
+neighbour (DHT_Node.py:491-510).  `validations` is advanced by the engine's own
+search-node counter (the naive-DFS count is not defined for a propagating
+search).
+"""
+import threading
+
+import numpy as np
+
+from .engine import SudokuEngine, encode_solve_grid, range_to_mask
+from .utils import split_array_in_middle
+from . import _lib as L
+
+_engines = {}
+_engines_lock = threading.Lock()
+
+
+def default_engine(device=0):
+    with _engines_lock:
+        eng = _engines.get(device)
+        if eng is None:
+            eng = _engines[device] = SudokuEngine(device)
+        return eng
+
+
+def _empty_cells(puzzle):
+    return [(r, c) for r in range(9) for c in range(9) if puzzle[r][c] == 0]
+
+
+def solve_grid(puzzle, arr=range(1, 10), engine=None):
+    """Core drop-in: mutate `puzzle` like the reference solver and return (ok, work)."""
+    eng = engine or default_engine()
+    board = encode_solve_grid(puzzle)
+    mask = np.array([range_to_mask(arr)], dtype=np.uint16)
+    out, status, work = eng.solve_batch(board[None, :], mask, want_work=True)
+    st = int(status[0])
+    if st == L.SDK_BUDGET_HIT:
+        raise L.SudokuHipError("node budget exhausted (SDK_OPT_NODE_BUDGET); the reference would still be searching")
+    if st == L.SDK_SOLVED:
+        sol = out[0]
+        for r, c in _empty_cells(puzzle):
+            puzzle[r][c] = int(sol[9 * r + c])
+        return True, int(work[0])
+    return False, int(work[0])
+
+
+def solve_sudoku(puzzle, arr=range(1, 10), engine=None):
+    """Function form of the solve contract (no node attached)."""
+    return solve_grid(puzzle, arr, engine)[0]
+
+
+class HipSolveMixin:
+    """Mix into DHT_Node.DHTNode: `class Node(HipSolveMixin, DHTNode)`.
+
+    Replaces solve_sudoku(self, puzzle, uuid, arr=range(1, 10)) (DHT_Node.py:474)."""
+
+    sudoku_engine = None
+
+    def solve_sudoku(self, puzzle, uuid=None, arr=range(1, 10)):
+        if self.task == []:                                   # DHT_Node.py:481-482
+            return False
+        data, addr = self.non_blocking_receive()              # DHT_Node.py:485-488
+        if data:
+            self.handleMessage(data, addr)
+        if self.neighbor and self.neighborfree:               # DHT_Node.py:491-510
+            if not self.task_queue.empty():
+                task = self.task_queue.get()
+                self.send_data(task, self.neighbor)
+                self.neighborfree = False
+                self.neighbor_tasks.put(task)
+            elif len(arr) > 1:
+                first_half, arr = split_array_in_middle(arr)
+                task = {"method": "TASK", "sudoku": puzzle, "range": first_half, "uuid": uuid}
+                self.send_data(task, self.neighbor)
+                self.neighbor_tasks.put(task)
+                self.neighborfree = False
+        ok, work = solve_grid(puzzle, arr, self.sudoku_engine)
+        self.validations += work
+        return ok
+
+
+class HipSolveMixinMain:
+    """Mix into main.DHTNode: replaces solve_sudoku(self, puzzle, arr=range(1, 10)) (main.py:301)."""
+
+    sudoku_engine = None
+
+    def solve_sudoku(self, puzzle, arr=range(1, 10)):
+        if self.task == []:                                   # main.py:306-307
+            return False
+        data, addr = self.non_blocking_receive()              # main.py:308-311
+        if data:
+            self.handleMessage(data, addr)
+        if self.neighbor and self.neighborfree and len(arr) > 1:   # main.py:313-325
+            first_half, arr = split_array_in_middle(arr)
+            self.send_data({"method": "TASK", "sudoku": puzzle, "range": first_half}, self.neighbor)
+            self.neighborfree = False
+        ok, work = solve_grid(puzzle, arr, self.sudoku_engine)
+        self.validations += work
+        return ok

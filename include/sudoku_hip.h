@@ -1,0 +1,124 @@
+/*
+ * sudoku_hip.h -- C-ABI of libsudoku_hip.so, the MI355X (gfx950) Sudoku engine.
+ *
+ * The reference (jsturm-11/distributed_sudoku_solver) has no FFI: its hot path
+ * is two Python call contracts, which this ABI replaces (see INTEGRATION.md for
+ * the ctypes binding the reference side would add):
+ *
+ *   DHTNode.solve_sudoku(puzzle, uuid, arr=range(1,10)) -> bool
+ *       DHT_Node.py:474-538 (twin main.py:301-354), with find_next_empty
+ *       utils.py:14-25, is_valid utils.py:27-56 and the TASK digit range that
+ *       split_array_in_middle (utils.py:1-9) produces.
+ *       -> sdk_solve_batch / sdk_solve_batch_dev
+ *   Sudoku(grid).check() -> bool            sudoku.py:43-94
+ *       -> sdk_check_batch / sdk_check_batch_dev
+ *   (no reference counterpart)
+ *       -> sdk_count_solutions
+ *
+ * Conventions
+ *   - Boards are uint8_t[81], row-major, 0 = empty, 1..9 = given digit,
+ *     10..255 = an out-of-domain given that (as in the reference, where only
+ *     `== guess` comparisons happen) never conflicts with a digit.
+ *   - Every function returns SDK_OK (0) or a negative SDK_E* code; the message
+ *     of the last failure on the calling thread is sdk_last_error().  No C++
+ *     exception and no abort() crosses this boundary.
+ *   - An sdk_ctx binds one HIP device and one HIP stream.  Calls on one context
+ *     are serialised by an internal mutex; distinct contexts may be used from
+ *     different threads concurrently.
+ *   - Host-pointer calls are synchronous.  *_dev calls take device pointers,
+ *     enqueue on the context stream and return immediately (sdk_synchronize).
+ *     Device boards must be 16-byte aligned.
+ */
+#ifndef SUDOKU_HIP_H
+#define SUDOKU_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDK_ABI_VERSION 1
+
+/* return codes */
+#define SDK_OK        0
+#define SDK_EINVAL   -1   /* bad argument */
+#define SDK_EHIP     -2   /* HIP runtime failure (message in sdk_last_error) */
+#define SDK_ENOMEM   -3   /* device or host allocation failed */
+
+/* per-board solve status (int8_t) */
+#define SDK_SOLVED        1   /* out = lexicographically first completion          */
+#define SDK_UNSOLVABLE    0   /* out = input (the reference restores the grid)     */
+#define SDK_BUDGET_HIT   -2   /* node budget exhausted; out = input                */
+
+/* check verdict bits (uint8_t) */
+#define SDK_CHECK_OK        1u  /* intended Sudoku.check(): all 27 units pass     */
+#define SDK_CHECK_RAW_NAMEERROR 2u /* reference check() would raise NameError      */
+                                   /* (sudoku.py:68): rows ok, cols ok, box00 sum 45 */
+
+/* options for sdk_set_option */
+#define SDK_OPT_ORDER        1  /* SDK_ORDER_*                                        */
+#define SDK_OPT_NODE_BUDGET  2  /* max search nodes per board, 0 = unlimited          */
+#define SDK_OPT_WAVES_PER_CU 3  /* solver residency, 1..32 (default 16)               */
+
+#define SDK_ORDER_MRV_UNIQUE 0  /* MRV search for <=2 solutions; lex re-search if >=2 */
+#define SDK_ORDER_LEX        1  /* lowest-index branching after propagation            */
+
+typedef struct sdk_ctx sdk_ctx;
+
+int         sdk_abi_version(void);
+const char *sdk_last_error(void);
+int         sdk_device_count(int *count);
+
+int sdk_create(int device, sdk_ctx **out);
+int sdk_destroy(sdk_ctx *ctx);
+int sdk_set_option(sdk_ctx *ctx, int key, int64_t value);
+int sdk_get_option(sdk_ctx *ctx, int key, int64_t *value);
+
+/* ---- host-pointer batch API (synchronous) ------------------------------- */
+
+/* Replaces Sudoku.check() (sudoku.py:43-94) for n boards: verdict[i] gets
+ * SDK_CHECK_* bits, evaluated with the reference's literal per-unit rule
+ * `sum == 45 and len(set) == 9`. */
+int sdk_check_batch(sdk_ctx *ctx, const uint8_t *boards, uint8_t *verdict, size_t n);
+
+/* Replaces DHTNode.solve_sudoku (DHT_Node.py:474-538) for n boards.
+ *   first_cell_mask  nullable; bit d (1..9) = digit d may be tried at the
+ *                    lowest-index empty input cell (the TASK `range`); NULL =
+ *                    range(1,10) for every board.
+ *   out              lexicographically first completion (= the reference's
+ *                    row-major ascending-digit DFS result) when status == 1,
+ *                    else a copy of the input.
+ *   status           SDK_SOLVED / SDK_UNSOLVABLE / SDK_BUDGET_HIT.
+ *   work             nullable; search nodes spent per board (engine counter, not
+ *                    the reference's naive-DFS `validations`). */
+int sdk_solve_batch(sdk_ctx *ctx, const uint8_t *in, const uint16_t *first_cell_mask,
+                    uint8_t *out, int8_t *status, uint64_t *work, size_t n);
+
+/* Counts completions of one board (same constraint as the solver), stopping
+ * at `limit` (0 = no limit).  status as above. */
+int sdk_count_solutions(sdk_ctx *ctx, const uint8_t *board, uint64_t limit,
+                        uint64_t *count, int8_t *status);
+
+/* ---- device-pointer API (asynchronous on the context stream) ------------ */
+int sdk_dev_alloc(sdk_ctx *ctx, size_t bytes, void **dptr);
+int sdk_dev_free(sdk_ctx *ctx, void *dptr);
+int sdk_memcpy_h2d(sdk_ctx *ctx, void *dst, const void *src, size_t bytes);
+int sdk_memcpy_d2h(sdk_ctx *ctx, void *dst, const void *src, size_t bytes);
+int sdk_synchronize(sdk_ctx *ctx);
+
+int sdk_check_batch_dev(sdk_ctx *ctx, const void *d_boards, void *d_verdict, size_t n);
+int sdk_solve_batch_dev(sdk_ctx *ctx, const void *d_in, const void *d_first_cell_mask,
+                        void *d_out, void *d_status, void *d_work, size_t n);
+
+/* Kernel time accounting (HIP events on the context stream, bracketing every
+ * kernel launched by the *_dev / host calls since the last reset).  Valid
+ * after sdk_synchronize. */
+int sdk_timer_reset(sdk_ctx *ctx);
+int sdk_timer_read(sdk_ctx *ctx, double *total_ms, int64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SUDOKU_HIP_H */

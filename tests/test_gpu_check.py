@@ -1,0 +1,60 @@
+"""HIP checker vs the oracle (bit-exact verdict bytes) and vs the reference's fixtures."""
+import numpy as np
+import pytest
+
+from distributed_sudoku_solver_amd import synth, _lib as L
+from distributed_sudoku_solver_amd.sudoku import Sudoku
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_check_cases(engine, check_cases):
+    boards = np.array([c["board"] for c in check_cases], dtype=np.uint8)
+    v = engine.check_batch(boards)
+    for c, x in zip(check_cases, v):
+        assert bool(x & L.SDK_CHECK_OK) == c["intended"], c["name"]
+        assert ("NameError" if x & L.SDK_CHECK_RAW_NAMEERROR else "False") == c["raw"], c["name"]
+
+
+def test_sudoku_class_dropin(engine, check_cases):
+    for c in check_cases[:20]:
+        grid = [c["board"][9 * r: 9 * r + 9] for r in range(9)]
+        s = Sudoku(grid, engine=engine)
+        assert s.check() == c["intended"]
+        if c["raw"] == "NameError":
+            with pytest.raises(NameError):
+                s.check(raw=True)
+        else:
+            assert s.check(raw=True) is False
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 255, 256, 257, 511, 1000, 4099])
+def test_ragged_sizes(engine, n):
+    b, exp = synth.make_check_boards(n, seed=n)
+    assert (engine.check_batch(b) == exp).all()
+
+
+def test_random_values_vs_oracle(engine):
+    rng = np.random.default_rng(5)
+    parts = [rng.integers(0, 10, (20000, 81)), rng.integers(0, 256, (5000, 81)), rng.integers(0, 20, (20000, 81))]
+    b = np.concatenate(parts).astype(np.uint8)
+    # literal-rule boards: valid grids relabelled to {0..7,17}, {0,2..8,10}, etc.
+    sols, _ = synth.make_check_boards(3000, seed=3)
+    for mp in ({1: 0, 9: 10}, {1: 0, 2: 1, 3: 2, 4: 3, 5: 4, 6: 5, 7: 6, 8: 7, 9: 17},
+               {1: 0, 2: 1, 3: 2, 4: 3, 5: 4, 6: 5, 7: 6, 8: 8, 9: 16}, {9: 18}, {1: 0, 9: 255}):
+        lut = np.arange(256, dtype=np.uint8)
+        for k, v in mp.items():
+            lut[k] = v
+        b = np.concatenate([b, lut[sols]])
+    assert (engine.check_batch(b) == O.check_batch(b, threads=8)).all()
+
+
+def test_one_million_synthetic(engine):
+    b, exp = synth.make_check_boards(1 << 20, seed=1234)
+    v = engine.check_batch(b)
+    assert (v == exp).all()
+
+
+def test_empty_batch(engine):
+    assert engine.check_batch(np.zeros((0, 81), np.uint8)).shape == (0,)

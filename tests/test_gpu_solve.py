@@ -1,0 +1,173 @@
+"""HIP solver vs the reference fixtures and the oracle: bit-exact boards and statuses."""
+import numpy as np
+import pytest
+
+from distributed_sudoku_solver_amd import SudokuEngine, synth, _lib as L
+from distributed_sudoku_solver_amd.solver import HipSolveMixin, solve_sudoku
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ORDERS = [L.SDK_ORDER_MRV_UNIQUE, L.SDK_ORDER_LEX]
+
+
+@pytest.fixture(params=ORDERS, ids=["mrv_unique", "lex"])
+def ordered_engine(request, engine):
+    engine.set_option(L.SDK_OPT_ORDER, request.param)
+    yield engine
+    engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+
+
+def test_golden_solve_cases(ordered_engine, solve_cases):
+    puz = np.array([c["puzzle"] for c in solve_cases], dtype=np.uint8)
+    masks = np.array([O.range_mask(*c["range"]) for c in solve_cases], dtype=np.uint16)
+    out, st, work = ordered_engine.solve_batch(puz, masks, want_work=True)
+    for i, c in enumerate(solve_cases):
+        assert (st[i] == 1) == c["ok"], c["name"]
+        assert out[i].tolist() == (c["board"] if c["ok"] else c["puzzle"]), c["name"]
+        assert work[i] >= 1
+
+
+def test_dropin_mutates_like_reference(engine, solve_cases):
+    for c in solve_cases[:30]:
+        grid = [list(c["puzzle"][9 * r: 9 * r + 9]) for r in range(9)]
+        ok = solve_sudoku(grid, range(*c["range"]), engine=engine)
+        assert ok == c["ok"], c["name"]
+        assert [v for row in grid for v in row] == (c["board"] if c["ok"] else c["puzzle"]), c["name"]
+
+
+class _FakeNode(HipSolveMixin):
+    def __init__(self, engine):
+        import queue
+        self.task = {"uuid": 0}
+        self.neighbor = None
+        self.neighborfree = False
+        self.validations = 0
+        self.task_queue = queue.Queue()
+        self.neighbor_tasks = queue.Queue()
+        self.sudoku_engine = engine
+
+    def non_blocking_receive(self):
+        return None, None
+
+
+def test_dht_node_mixin(engine, solve_cases):
+    node = _FakeNode(engine)
+    c = next(x for x in solve_cases if x["name"] == "wiki")
+    grid = [list(c["puzzle"][9 * r: 9 * r + 9]) for r in range(9)]
+    assert node.solve_sudoku(grid, 0, range(1, 10)) is True
+    assert [v for row in grid for v in row] == c["board"]
+    assert node.validations > 0
+    node.task = []
+    assert node.solve_sudoku(grid, 0, range(1, 10)) is False     # cancellation, DHT_Node.py:481
+
+
+def _random_puzzles(n, seed, lo_clues, hi_clues):
+    rng = np.random.default_rng(seed)
+    _, sol = synth.make_17clue(n, seed=seed)
+    keep = rng.random((n, 81)) < rng.uniform(lo_clues, hi_clues, (n, 1)) / 81.0
+    return np.where(keep, sol, 0).astype(np.uint8)
+
+
+def test_random_multi_solution_boards_vs_oracle(ordered_engine):
+    """Sparse boards have many completions: the lexicographically first one must be returned."""
+    puz = _random_puzzles(400, 21, 8, 30)
+    rng = np.random.default_rng(22)
+    lo = rng.integers(1, 10, len(puz))
+    hi = np.minimum(10, lo + rng.integers(1, 10, len(puz)))
+    masks = np.array([O.range_mask(a, b) for a, b in zip(lo, hi)], dtype=np.uint16)
+    out, st, _ = ordered_engine.solve_batch(puz, masks)
+    ref_out, ref_st, _ = O.naive_solve_batch(puz, masks, budget=50_000_000, threads=8)
+    done = ref_st != -2
+    assert done.mean() > 0.9
+    assert (st[done] == ref_st[done]).all()
+    assert (out[done] == ref_out[done]).all()
+
+
+def test_conflicting_and_inert_givens_vs_oracle(ordered_engine):
+    rng = np.random.default_rng(31)
+    puz = _random_puzzles(600, 31, 20, 45)
+    n = len(puz)
+    for i in range(n):
+        nz = np.flatnonzero(puz[i])
+        if i % 3 == 0 and len(nz) >= 2:          # plant a given-vs-given duplicate
+            a, b = rng.choice(nz, 2, replace=False)
+            puz[i, b] = puz[i, a]
+        elif i % 3 == 1:                          # plant out-of-domain givens
+            cells = rng.choice(81, 2, replace=False)
+            puz[i, cells] = rng.integers(10, 256, 2)
+    out, st, _ = ordered_engine.solve_batch(puz)
+    ref_out, ref_st, _ = O.naive_solve_batch(puz, budget=20_000_000, threads=8)
+    done = ref_st != -2
+    assert done.mean() > 0.8
+    assert (st[done] == ref_st[done]).all()
+    assert (out[done] == ref_out[done]).all()
+
+
+def test_17_clue_transforms_exact(engine):
+    p, s = synth.make_17clue(20000, seed=99)
+    out, st, work = engine.solve_batch(p, want_work=True)
+    assert (st == 1).all()
+    assert (out == s).all()
+    assert (O.check_batch(out, 8) == 3).all()       # every output passes the reference check()
+
+
+def test_30_clue_exact(engine):
+    p, s = synth.make_30clue(50000, seed=98)
+    out, st, _ = engine.solve_batch(p)
+    assert (st == 1).all() and (out == s).all()
+
+
+def test_lex_and_mrv_orders_agree_on_seeds(engine):
+    p, s = synth.seed_arrays()
+    for order in ORDERS:
+        engine.set_option(L.SDK_OPT_ORDER, order)
+        out, st, _ = engine.solve_batch(p)
+        assert (st == 1).all() and (out == s).all()
+    engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+
+
+def test_unsolvable_and_edge_boards(engine):
+    boards = []
+    b = np.zeros(81, np.uint8); b[0] = b[1] = 5              # '55' + 79 zeros: provably unsolvable
+    boards.append(b)
+    boards.append(np.zeros(81, np.uint8))                      # empty board
+    full = synth.parse(synth.WIKI_SOLUTION).copy(); boards.append(full)
+    dup = full.copy(); dup[10] = dup[0]; boards.append(dup)    # full board with a given conflict -> True
+    bad = synth.parse(synth.WIKI).copy(); bad[2] = 5           # wiki with a conflicting given
+    boards.append(bad)
+    out, st, _ = engine.solve_batch(np.stack(boards))
+    assert st.tolist() == [0, 1, 1, 1, 0]
+    assert out[2].tolist() == full.tolist() and out[3].tolist() == dup.tolist()
+    assert out[0].tolist() == boards[0].tolist() and out[4].tolist() == bad.tolist()
+    ref = O.naive_solve(boards[1])
+    assert out[1].tolist() == ref[1]
+
+
+def test_budget_status(engine):
+    engine.set_option(L.SDK_OPT_NODE_BUDGET, 1)
+    p, _ = synth.seed_arrays()
+    b = np.zeros(81, np.uint8); b[0] = b[1] = 5
+    out, st, _ = engine.solve_batch(np.concatenate([p, b[None]]))
+    engine.set_option(L.SDK_OPT_NODE_BUDGET, 0)
+    assert (st == -2).any()
+    assert (out[st == -2] == np.concatenate([p, b[None]])[st == -2]).all()
+
+
+def test_count_solutions(engine):
+    s1 = synth.SEEDS17["S1"]
+    b16 = synth.parse(s1[:-9] + "000800000")
+    assert engine.count_solutions(b16) == (7309, 1)
+    assert engine.count_solutions(b16, limit=100) == (100, 1)
+    p, _ = synth.seed_arrays()
+    for i in range(5):
+        assert engine.count_solutions(p[i]) == (1, 1)
+    rng = np.random.default_rng(3)
+    puz = _random_puzzles(30, 41, 22, 30)
+    for b in puz:
+        assert engine.count_solutions(b, limit=5000)[0] == O.count(b, 5000, 1)
+
+
+def test_empty_batch(engine):
+    out, st, _ = engine.solve_batch(np.zeros((0, 81), np.uint8))
+    assert out.shape == (0, 81) and st.shape == (0,)

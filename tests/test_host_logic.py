@@ -1,0 +1,66 @@
+"""Host-side boundary logic: grid encoding, TASK range -> mask, synthetic workloads."""
+import numpy as np
+import pytest
+
+from distributed_sudoku_solver_amd import engine as E, synth
+from distributed_sudoku_solver_amd.utils import split_array_in_middle
+from oracle import oracle as O
+
+
+def test_encode_solve_grid_follows_reference_equality():
+    g = [[0] * 9 for _ in range(9)]
+    g[0][0], g[0][1], g[0][2], g[0][3], g[0][4] = 5, 5.0, True, 10, 2.5
+    g[1][0], g[1][1] = -3, 0.0
+    b = E.encode_solve_grid(g)
+    assert b[:5].tolist() == [5, 5, 1, 10, 10]
+    assert b[9] == 10 and b[10] == 0
+
+
+def test_encode_check_grid_domain():
+    g = [[1] * 9 for _ in range(9)]
+    g[0][0] = 255
+    assert E.encode_check_grid(g)[0] == 255
+    g[0][0] = 256
+    with pytest.raises(ValueError):
+        E.encode_check_grid(g)
+
+
+def test_range_to_mask_matches_split_semantics():
+    assert E.range_to_mask(range(1, 10)) == 0x3FE
+    a, b = split_array_in_middle(range(1, 10))
+    assert (E.range_to_mask(a), E.range_to_mask(b)) == (0b11110, 0b1111100000)
+    assert E.range_to_mask(a) | E.range_to_mask(b) == 0x3FE
+    assert E.range_to_mask(range(5, 5)) == 0
+    assert E.range_to_mask(range(0, 3)) == 0b110
+    assert E.range_to_mask([2, 4, 7]) == (1 << 2) | (1 << 4) | (1 << 7)
+    for bad in ([3, 1], range(1, 11), [-1]):
+        with pytest.raises(ValueError):
+            E.range_to_mask(bad)
+    for lo in range(1, 10):
+        for hi in range(lo, 11):
+            assert E.range_to_mask(range(lo, hi)) == O.range_mask(lo, hi)
+
+
+def test_split_array_in_middle():
+    assert split_array_in_middle(range(1, 10)) == (range(1, 5), range(5, 10))
+    assert split_array_in_middle(range(9, 10)) == (range(9, 9), range(9, 10))
+
+
+def test_synth_17clue_is_unique_and_consistent():
+    p, s = synth.make_17clue(2000, seed=7)
+    assert ((p > 0).sum(1) == 17).all()
+    assert ((p == 0) | (p == s)).all()
+    assert (O.check_batch(s, 4) == 3).all()
+    for i in range(0, 2000, 400):
+        assert O.count(p[i], 2, 1) == 1
+    # deterministic for a seed
+    p2, _ = synth.make_17clue(2000, seed=7)
+    assert (p == p2).all()
+
+
+def test_synth_30clue_and_check_boards():
+    p, s = synth.make_30clue(2000, seed=9)
+    assert ((p > 0).sum(1) == 30).all() and ((p == 0) | (p == s)).all()
+    b, exp = synth.make_check_boards(20000, seed=11)
+    assert (O.check_batch(b, 4) == exp).all()
+    assert 0.45 < (exp == 3).mean() < 0.55

@@ -118,8 +118,12 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel(const uint8_t* __r
                 tile[(kCheckTileVec / kCheckThreads) * kCheckThreads + t] =
                     __builtin_nontemporal_load(&s4[(kCheckTileVec / kCheckThreads) * kCheckThreads + t]);
         } else {
+            // ragged last tile: each thread copies its own record byte by byte
             uint8_t* tb = reinterpret_cast<uint8_t*>(tile);
-            for (uint64_t j = t; j < cnt * 81; j += kCheckThreads) tb[j] = src[j];
+            if ((uint64_t)t < cnt) {
+#pragma unroll
+                for (int k = 0; k < 81; ++k) tb[81 * t + k] = src[81 * t + k];
+            }
         }
         __syncthreads();
         if ((uint64_t)t < cnt)

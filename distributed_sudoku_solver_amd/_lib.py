@@ -45,6 +45,9 @@ SIGNATURES = {
     "sdk_solve_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz]),
     "sdk_count_solutions": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.POINTER(ctypes.c_int8)]),
+    "sdk_count_solutions_slice": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                                 ctypes.POINTER(ctypes.c_int8)]),
     "sdk_dev_alloc": (ctypes.c_int, [_vp, _sz, ctypes.POINTER(_vp)]),
     "sdk_dev_free": (ctypes.c_int, [_vp, _vp]),
     "sdk_memcpy_h2d": (ctypes.c_int, [_vp, _vp, _vp, _sz]),

@@ -1,0 +1,150 @@
+// frontier_kernel.h -- breadth-first frontier expansion for whole-tree searches
+// (solution counting).
+//
+// One expansion level turns a frontier of boards into the boards of their
+// children, deterministically (same order on every GPU, so a replicated
+// frontier can be sliced across GPUs without an exchange):
+//   expand_kernel  one wave per board: propagate (solve_kernel.h), then
+//                  CONTRA -> 0 children; SOLVED -> 0 children and one leaf;
+//                  OPEN -> branch on the MRV cell, nchild = #candidates.  The
+//                  propagated board is written back with every single-valued
+//                  cell as a given (a fixpoint has no conflict among them, so
+//                  treating them as givens changes no completion).
+//   scan_kernel    exclusive prefix sum of nchild (one 1024-thread workgroup,
+//                  wave-level __shfl_up scans + LDS for the wave totals).
+//   emit_kernel    one wave per parent writes its children contiguously at
+//                  offset[parent], digits ascending: children of one parent
+//                  and parents in order -> a coalesced, ordered HBM array.
+#pragma once
+#include "solve_kernel.h"
+
+namespace sdk {
+
+struct ExpandArgs {
+    const uint8_t* in;
+    uint64_t m;
+    uint8_t* prop;            // [m][81] propagated board (singles as givens)
+    uint8_t* bcell;           // [m] branch cell
+    uint16_t* bmask;          // [m] branch candidates (bit d-1 = digit d)
+    uint32_t* nchild;         // [m]
+    unsigned long long* leaves;
+    uint32_t* next;
+    int order;
+};
+
+__device__ __forceinline__ uint32_t board_byte(uint32_t in, uint32_t s) {
+    // givens keep their byte; single-valued cells become givens; open cells stay 0
+    if (in) return in;
+    const uint32_t v = s & kCands;
+    return is_single(v) ? (uint32_t)__ffs(v) : 0u;
+}
+
+__global__ __launch_bounds__(64) void expand_kernel(ExpandArgs a) {
+    __shared__ uint32_t s_cell[96];
+    __shared__ uint32_t s_unit[32];
+    __shared__ uint32_t s_br[4];
+    Wave w;
+    init_wave(w, s_cell, s_unit, s_br);
+    const int lane = w.lane;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(a.next, kChunk);
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        if ((uint64_t)base >= a.m) break;
+        const uint64_t end = min((uint64_t)base + kChunk, a.m);
+        for (uint64_t i = base; i < end; ++i) {
+            const uint8_t* src = a.in + i * 81;
+            const uint32_t inA = src[lane];
+            const uint32_t inB = w.hasB ? (uint32_t)src[64 + lane] : 0u;
+            uint32_t sa = cell_init(inA);
+            uint32_t sb = w.hasB ? cell_init(inB) : kInert;
+            const int r = propagate(w, sa, sb);
+            uint32_t nch = 0, cell = 0, m = 0;
+            if (r == P_SOLVED) {
+                if (lane == 0) atomicAdd(a.leaves, 1ull);
+            } else if (r == P_OPEN) {
+                const uint32_t pa = open_count(sa);
+                const uint32_t pb = w.hasB ? open_count(sb) : 0u;
+                unsigned long long ma, mb;
+                if (a.order == ORDER_LEX) {
+                    ma = __ballot(pa >= 2);
+                    mb = __ballot(pb >= 2);
+                } else {
+                    ma = mb = 0;
+                    for (uint32_t k = 2; k <= 9; ++k) {
+                        ma = __ballot(pa == k);
+                        mb = __ballot(pb == k);
+                        if (ma | mb) break;
+                    }
+                }
+                cell = ma ? (uint32_t)__builtin_ctzll(ma) : 64u + (uint32_t)__builtin_ctzll(mb);
+                const uint32_t src_s = cell < 64 ? sa : sb;
+                m = (uint32_t)__builtin_amdgcn_readlane((int)src_s, (int)(cell & 63)) & kCands;
+                nch = (uint32_t)__popc(m);
+                uint8_t* dst = a.prop + i * 81;
+                dst[lane] = (uint8_t)board_byte(inA, sa);
+                if (w.hasB) dst[64 + lane] = (uint8_t)board_byte(inB, sb);
+            }
+            if (lane == 0) {
+                a.nchild[i] = nch;
+                a.bcell[i] = (uint8_t)cell;
+                a.bmask[i] = (uint16_t)m;
+            }
+        }
+    }
+}
+
+// Exclusive scan of n uint32 counts into uint64 offsets; total written to *total.
+__global__ __launch_bounds__(1024) void scan_kernel(const uint32_t* __restrict__ cnt, uint64_t* __restrict__ off,
+                                                     uint64_t n, unsigned long long* total) {
+    __shared__ uint64_t s_wave[16];
+    __shared__ uint64_t s_carry;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) s_carry = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < n; base += 1024) {
+        const uint64_t i = base + t;
+        const uint64_t x = i < n ? cnt[i] : 0;
+        uint64_t inc = x;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(inc, d);
+            if (lane >= d) inc += y;
+        }
+        if (lane == 63) s_wave[wv] = inc;
+        __syncthreads();
+        uint64_t wbase = 0;
+        for (int k = 0; k < wv; ++k) wbase += s_wave[k];
+        const uint64_t carry = s_carry;
+        if (i < n) off[i] = carry + wbase + inc - x;
+        __syncthreads();
+        if (t == 1023) s_carry = carry + wbase + inc;
+        __syncthreads();
+    }
+    if (t == 0) *total = s_carry;
+}
+
+__global__ __launch_bounds__(64) void emit_kernel(const uint8_t* __restrict__ prop, const uint8_t* __restrict__ bcell,
+                                                  const uint16_t* __restrict__ bmask, const uint64_t* __restrict__ off,
+                                                  uint64_t m, uint8_t* __restrict__ out) {
+    const int lane = threadIdx.x;
+    const bool hasB = lane < 17;
+    for (uint64_t i = blockIdx.x; i < m; i += gridDim.x) {
+        uint32_t mask = bmask[i];
+        if (!mask) continue;
+        const uint32_t cell = bcell[i];
+        const uint32_t a = prop[i * 81 + lane];
+        const uint32_t b = hasB ? prop[i * 81 + 64 + lane] : 0u;
+        uint64_t j = off[i];
+        while (mask) {
+            const uint32_t d = (uint32_t)__ffs(mask);  // digit
+            mask &= mask - 1;
+            uint8_t* dst = out + j * 81;
+            dst[lane] = (uint8_t)((uint32_t)lane == cell ? d : a);
+            if (hasB) dst[64 + lane] = (uint8_t)((uint32_t)(64 + lane) == cell ? d : b);
+            ++j;
+        }
+    }
+}
+
+}  // namespace sdk

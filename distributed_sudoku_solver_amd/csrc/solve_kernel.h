@@ -65,8 +65,9 @@ struct SolveArgs {
     uint32_t* stack;           // gridDim.x * kStackWordsPerBlock words
     uint64_t budget;           // nodes per board, 0 = unlimited
     int order;                 // SDK_ORDER_*
-    uint64_t limit;            // count mode only
-    unsigned long long* count; // count mode only
+    uint64_t limit;            // count mode: per-board completion limit (0 = none)
+    unsigned long long* count; // count mode: running total over the batch (atomic)
+    unsigned long long* counts;// count mode: per-board counts (nullable)
     int count_mode;
 };
 
@@ -239,40 +240,44 @@ __device__ int64_t search(const Wave& w, int order, uint32_t sa0, uint32_t sb0, 
     }
 }
 
+__device__ __forceinline__ void init_wave(Wave& w, uint32_t* s_cell, uint32_t* s_unit, uint32_t* s_br) {
+    w.s_cell = s_cell;
+    w.s_unit = s_unit;
+    w.s_br = s_br;
+    w.stk = nullptr;
+    const int lane = threadIdx.x;
+    w.lane = lane;
+    w.hasB = lane < 17;
+    const int c = lane;
+    w.uA0 = c / 9;
+    w.uA1 = 9 + c % 9;
+    w.uA2 = 18 + (c / 27) * 3 + (c % 9) / 3;
+    const int cb = w.hasB ? 64 + lane : 0;
+    w.uB0 = cb / 9;
+    w.uB1 = 9 + cb % 9;
+    w.uB2 = 18 + (cb / 27) * 3 + (cb % 9) / 3;
+    const int u = lane < 27 ? lane : 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        int cell;
+        if (u < 9) cell = 9 * u + k;
+        else if (u < 18) cell = 9 * k + (u - 9);
+        else {
+            const int b = u - 18;
+            cell = ((b / 3) * 3 + k / 3) * 9 + (b % 3) * 3 + k % 3;
+        }
+        w.ucell[k] = cell;
+    }
+}
+
 __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     __shared__ uint32_t s_cell[96];
     __shared__ uint32_t s_unit[32];
     __shared__ uint32_t s_br[kMaxDepth];
     Wave w;
-    w.s_cell = s_cell;
-    w.s_unit = s_unit;
-    w.s_br = s_br;
+    init_wave(w, s_cell, s_unit, s_br);
     w.stk = a.stack + (size_t)blockIdx.x * kStackWordsPerBlock;
-    const int lane = threadIdx.x;
-    w.lane = lane;
-    w.hasB = lane < 17;
-    {
-        const int c = lane;
-        w.uA0 = c / 9;
-        w.uA1 = 9 + c % 9;
-        w.uA2 = 18 + (c / 27) * 3 + (c % 9) / 3;
-        const int cb = w.hasB ? 64 + lane : 0;
-        w.uB0 = cb / 9;
-        w.uB1 = 9 + cb % 9;
-        w.uB2 = 18 + (cb / 27) * 3 + (cb % 9) / 3;
-        const int u = lane < 27 ? lane : 0;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            int cell;
-            if (u < 9) cell = 9 * u + k;
-            else if (u < 18) cell = 9 * k + (u - 9);
-            else {
-                const int b = u - 18;
-                cell = ((b / 3) * 3 + k / 3) * 9 + (b % 3) * 3 + k % 3;
-            }
-            w.ucell[k] = cell;
-        }
-    }
+    const int lane = w.lane;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(a.next, kChunk);
@@ -294,14 +299,27 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
             } else if (zb) {
                 if (lane == (int)__builtin_ctzll(zb)) sb &= fm | ~kCands;
             }
-            uint8_t* dst = a.out + i * 81;
+            uint8_t* dst = a.out ? a.out + i * 81 : nullptr;
             uint64_t nodes = 0;
             int8_t st;
             if (a.count_mode) {
-                const int64_t c = search(w, ORDER_MRV, sa, sb, a.limit, a.budget, nodes, dst, inA, inB);
-                if (lane == 0) *a.count = (unsigned long long)(c < 0 ? 0 : c);
+                // whole-subtree count (order-independent, so MRV); the batch stops
+                // early once the running total reaches the limit
+                int64_t c = 0;
+                bool skip = false;
+                if (a.limit) {
+                    unsigned long long tot = 0;
+                    if (lane == 0) tot = __hip_atomic_load(a.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    tot = __shfl(tot, 0);
+                    skip = tot >= a.limit;
+                }
+                if (!skip) c = search(w, ORDER_MRV, sa, sb, a.limit, a.budget, nodes, a.out ? dst : nullptr, inA, inB);
+                if (lane == 0) {
+                    if (c > 0) atomicAdd(a.count, (unsigned long long)c);
+                    if (a.counts) a.counts[i] = (unsigned long long)(c < 0 ? 0 : c);
+                }
                 st = c < 0 ? (int8_t)-2 : (c > 0 ? (int8_t)1 : (int8_t)0);
-                if (c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
+                if (a.out && c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
             } else {
                 int64_t c;
                 if (a.order == ORDER_LEX) {
@@ -314,7 +332,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
                 if (c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
             }
             if (lane == 0) {
-                a.status[i] = st;
+                if (a.status) a.status[i] = st;
                 if (a.work) a.work[i] = nodes;
             }
         }

@@ -17,6 +17,7 @@
 #include "../../include/sudoku_hip.h"
 #include "check_kernel.h"
 #include "solve_kernel.h"
+#include "frontier_kernel.h"
 
 namespace {
 
@@ -58,6 +59,7 @@ struct sdk_ctx {
     int waves_per_cu = 16;
     // workspaces
     DevBuf stack, counter, in, mask, out, status, work, verdict;
+    DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status;
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     size_t events_used = 0;
@@ -104,7 +106,8 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
 }
 
 int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
-                 uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count) {
+                 uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
+                 unsigned long long* d_counts = nullptr) {
     if (n == 0) return SDK_OK;
     if (n > 0x7FFFFFFFull) return fail(SDK_EINVAL, "at most 2^31-1 boards per call");
     const uint64_t want = (n + sdk::kChunk - 1) / sdk::kChunk;
@@ -113,7 +116,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     if (rc) return rc;
     rc = ensure(c->counter, 256);
     if (rc) return rc;
-    HIPCALL(hipMemsetAsync(c->counter.p, 0, 256, c->stream));
+    HIPCALL(hipMemsetAsync(c->counter.p, 0, 8, c->stream));  // word 0 = work counter; words 1.. belong to callers
     sdk::SolveArgs a;
     a.in = d_in;
     a.mask = d_mask;
@@ -127,6 +130,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.order = c->order;
     a.limit = limit;
     a.count = d_count;
+    a.counts = d_counts;
     a.count_mode = count_mode;
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
@@ -134,6 +138,101 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     sdk::solve_kernel<<<grid, 64, 0, c->stream>>>(a);
     HIPCALL(hipGetLastError());
     HIPCALL(hipEventRecord(stop, c->stream));
+    return SDK_OK;
+}
+
+// Whole-tree solution count with a replicated, deterministic BFS frontier.
+// Every rank expands the same frontier (no exchange), counts the subtrees of its
+// contiguous slice with the batched count kernel; rank 0 also owns the leaves
+// solved during expansion.  The caller sums the per-rank counts.
+int count_frontier(sdk_ctx* c, const uint8_t* h_board, uint64_t limit, int rank, int world, uint64_t* local_count,
+                   uint64_t* frontier_size, int8_t* status) {
+    if (world < 1 || rank < 0 || rank >= world) return fail(SDK_EINVAL, "bad rank %d / world %d", rank, world);
+    int rc;
+    // counters: [0] next (u32), [1] leaves (u64), [2] scan total (u64), [3] count total (u64)
+    if ((rc = ensure(c->counter, 256)) || (rc = ensure(c->fr_a, 81))) return rc;
+    unsigned long long* ctr = static_cast<unsigned long long*>(c->counter.p);
+    unsigned long long* d_leaves = ctr + 1;
+    unsigned long long* d_total = ctr + 2;
+    unsigned long long* d_count = ctr + 3;
+    HIPCALL(hipMemsetAsync(c->counter.p, 0, 256, c->stream));
+    HIPCALL(hipMemcpyAsync(c->fr_a.p, h_board, 81, hipMemcpyHostToDevice, c->stream));
+    const uint64_t target = (uint64_t)c->cus * (uint64_t)c->waves_per_cu * 8ull * (uint64_t)world;
+    const uint64_t cap = 1ull << 25;  // 32M boards (2.6 GB) per frontier buffer
+    uint64_t m = 1;
+    int level = 0;
+    while (m > 0 && m < target && level < 81) {
+        if ((rc = ensure(c->prop, m * 81)) || (rc = ensure(c->bcell, m)) || (rc = ensure(c->bmask, m * 2)) ||
+            (rc = ensure(c->nchild, m * 4)) || (rc = ensure(c->offs, m * 8)))
+            return rc;
+        HIPCALL(hipMemsetAsync(c->counter.p, 0, 4, c->stream));
+        sdk::ExpandArgs ea;
+        ea.in = static_cast<const uint8_t*>(c->fr_a.p);
+        ea.m = m;
+        ea.prop = static_cast<uint8_t*>(c->prop.p);
+        ea.bcell = static_cast<uint8_t*>(c->bcell.p);
+        ea.bmask = static_cast<uint16_t*>(c->bmask.p);
+        ea.nchild = static_cast<uint32_t*>(c->nchild.p);
+        ea.leaves = d_leaves;
+        ea.next = static_cast<uint32_t*>(c->counter.p);
+        ea.order = sdk::ORDER_MRV;
+        const unsigned eg = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m + sdk::kChunk - 1) / sdk::kChunk,
+                                                                               (uint64_t)c->cus * c->waves_per_cu));
+        hipEvent_t stop;
+        if ((rc = timer_begin(c, &stop))) return rc;
+        sdk::expand_kernel<<<eg, 64, 0, c->stream>>>(ea);
+        HIPCALL(hipGetLastError());
+        sdk::scan_kernel<<<1, 1024, 0, c->stream>>>(static_cast<uint32_t*>(c->nchild.p),
+                                                    static_cast<uint64_t*>(c->offs.p), m, d_total);
+        HIPCALL(hipGetLastError());
+        unsigned long long total = 0;
+        HIPCALL(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCALL(hipStreamSynchronize(c->stream));
+        if (total > cap) {
+            HIPCALL(hipEventRecord(stop, c->stream));
+            break;  // keep the current frontier: it is already big enough to split
+        }
+        if (total && (rc = ensure(c->fr_b, total * 81))) return rc;
+        if (total) {
+            const unsigned gg = (unsigned)std::min<uint64_t>(m, (uint64_t)c->cus * 32);
+            sdk::emit_kernel<<<gg, 64, 0, c->stream>>>(static_cast<uint8_t*>(c->prop.p), static_cast<uint8_t*>(c->bcell.p),
+                                                       static_cast<uint16_t*>(c->bmask.p),
+                                                       static_cast<uint64_t*>(c->offs.p), m,
+                                                       static_cast<uint8_t*>(c->fr_b.p));
+            HIPCALL(hipGetLastError());
+        }
+        HIPCALL(hipEventRecord(stop, c->stream));
+        std::swap(c->fr_a, c->fr_b);
+        m = total;
+        ++level;
+    }
+    // count this rank's slice of the final frontier
+    const uint64_t lo = (rank * m) / world, hi = ((rank + 1) * m) / world;
+    int8_t st = 1;
+    uint64_t cnt = 0;
+    if (hi > lo) {
+        if ((rc = ensure(c->fr_status, hi - lo))) return rc;
+        rc = launch_solve(c, static_cast<uint8_t*>(c->fr_a.p) + lo * 81, nullptr, nullptr,
+                          static_cast<int8_t*>(c->fr_status.p), nullptr, hi - lo, 1, limit, d_count, nullptr);
+        if (rc) return rc;
+        std::vector<int8_t> sts(hi - lo);
+        HIPCALL(hipMemcpyAsync(sts.data(), c->fr_status.p, hi - lo, hipMemcpyDeviceToHost, c->stream));
+        unsigned long long tot = 0;
+        HIPCALL(hipMemcpyAsync(&tot, d_count, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCALL(hipStreamSynchronize(c->stream));
+        cnt = tot;
+        for (int8_t x : sts)
+            if (x == -2) st = -2;
+    }
+    unsigned long long leaves = 0;
+    HIPCALL(hipMemcpyAsync(&leaves, d_leaves, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    if (rank == 0) cnt += leaves;
+    if (limit && cnt > limit) cnt = limit;
+    if (st != -2) st = cnt > 0 ? 1 : 0;
+    *local_count = cnt;
+    if (frontier_size) *frontier_size = m;
+    *status = st;
     return SDK_OK;
 }
 
@@ -182,7 +281,8 @@ int sdk_destroy(sdk_ctx* c) {
     if (!c) return SDK_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->stack, &c->counter, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict})
+    for (DevBuf* b : {&c->stack, &c->counter, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
+                      &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status})
         if (b->p) (void)hipFree(b->p);
     for (auto& pr : c->events) {
         (void)hipEventDestroy(pr.first);
@@ -350,23 +450,15 @@ int sdk_count_solutions(sdk_ctx* c, const uint8_t* board, uint64_t limit, uint64
     if (!c || !board || !count || !status) return fail(SDK_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
-    int rc;
-    if ((rc = ensure(c->in, 81)) || (rc = ensure(c->out, 81)) || (rc = ensure(c->status, 8)) ||
-        (rc = ensure(c->work, 16)))
-        return rc;
-    HIPCALL(hipMemcpyAsync(c->in.p, board, 81, hipMemcpyHostToDevice, c->stream));
-    unsigned long long* d_count = static_cast<unsigned long long*>(c->work.p) + 1;
-    rc = launch_solve(c, static_cast<uint8_t*>(c->in.p), nullptr, static_cast<uint8_t*>(c->out.p),
-                      static_cast<int8_t*>(c->status.p), static_cast<uint64_t*>(c->work.p), 1, 1, limit, d_count);
-    if (rc) return rc;
-    unsigned long long cnt = 0;
-    int8_t st = 0;
-    HIPCALL(hipMemcpyAsync(&cnt, d_count, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCALL(hipMemcpyAsync(&st, c->status.p, 1, hipMemcpyDeviceToHost, c->stream));
-    HIPCALL(hipStreamSynchronize(c->stream));
-    *count = cnt;
-    *status = st;
-    return SDK_OK;
+    return count_frontier(c, board, limit, 0, 1, count, nullptr, status);
+}
+
+int sdk_count_solutions_slice(sdk_ctx* c, const uint8_t* board, uint64_t limit, int rank, int world,
+                              uint64_t* count, uint64_t* frontier_size, int8_t* status) {
+    if (!c || !board || !count || !status) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    return count_frontier(c, board, limit, rank, world, count, frontier_size, status);
 }
 
 }  // extern "C"

@@ -197,6 +197,17 @@ class SudokuEngine:
                 "sdk_count_solutions")
         return cnt.value, st.value
 
+    def count_solutions_slice(self, board, rank, world, limit=0):
+        """This rank's share of a frontier-split count: (local_count, frontier_size, status)."""
+        board = np.ascontiguousarray(board, dtype=np.uint8).reshape(81)
+        cnt = ctypes.c_uint64()
+        fr = ctypes.c_uint64()
+        st = ctypes.c_int8()
+        L.check(self.lib.sdk_count_solutions_slice(self.ctx, _ptr(board), int(limit), int(rank), int(world),
+                                                   ctypes.byref(cnt), ctypes.byref(fr), ctypes.byref(st)),
+                "sdk_count_solutions_slice")
+        return cnt.value, fr.value, st.value
+
     # --------------------------------------------------------- device batch
     def check_batch_dev(self, d_boards, d_verdict, n):
         L.check(self.lib.sdk_check_batch_dev(self.ctx, d_boards.ptr, d_verdict.ptr, int(n)), "sdk_check_batch_dev")

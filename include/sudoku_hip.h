@@ -101,6 +101,14 @@ int sdk_solve_batch(sdk_ctx *ctx, const uint8_t *in, const uint16_t *first_cell_
 int sdk_count_solutions(sdk_ctx *ctx, const uint8_t *board, uint64_t limit,
                         uint64_t *count, int8_t *status);
 
+/* Multi-GPU form (one context per GPU, one call per rank): every rank expands
+ * the same deterministic breadth-first frontier of `board` and counts the
+ * subtrees of its contiguous slice; rank 0 also counts the completions met
+ * during expansion.  The sum of `count` over ranks is the total (callers
+ * all-reduce it).  frontier_size (nullable) = boards in the split frontier. */
+int sdk_count_solutions_slice(sdk_ctx *ctx, const uint8_t *board, uint64_t limit, int rank, int world,
+                              uint64_t *count, uint64_t *frontier_size, int8_t *status);
+
 /* ---- device-pointer API (asynchronous on the context stream) ------------ */
 int sdk_dev_alloc(sdk_ctx *ctx, size_t bytes, void **dptr);
 int sdk_dev_free(sdk_ctx *ctx, void *dptr);

@@ -179,3 +179,24 @@ def test_count_solutions(engine):
 def test_empty_batch(engine):
     out, st, _ = engine.solve_batch(np.zeros((0, 81), np.uint8))
     assert out.shape == (0, 81) and st.shape == (0,)
+
+
+def test_frontier_count_matches_oracle_and_slices_partition(engine):
+    from distributed_sudoku_solver_amd.shard import sharded_count
+    s1 = synth.SEEDS17["S1"]
+    b16 = synth.parse(s1[:-9] + "000800000")
+    b15 = synth.parse(s1[:-9] + "0" * 9)
+    assert engine.count_solutions(b15) == (3481026, 1)
+    for world in (2, 3, 8):
+        parts = [engine.count_solutions_slice(b16, r, world) for r in range(world)]
+        assert sum(p[0] for p in parts) == 7309
+        assert len({p[1] for p in parts}) == 1            # same replicated frontier on every rank
+    assert sharded_count(engine, b16, 0, 1) [:2] == (7309, 1)
+    # sparse boards vs the oracle's counter
+    puz = _random_puzzles(20, 77, 24, 32)
+    for b in puz:
+        assert engine.count_solutions(b)[0] == O.count(b, 0, 1)
+    # no completion / limit
+    dead = synth.parse(synth.WIKI).copy(); dead[2] = 5
+    assert engine.count_solutions(dead) == (0, 0)
+    assert engine.count_solutions(b15, limit=1000)[0] == 1000

@@ -26,6 +26,7 @@ SDK_CHECK_RAW_NAMEERROR = 2
 SDK_OPT_ORDER = 1
 SDK_OPT_NODE_BUDGET = 2
 SDK_OPT_WAVES_PER_CU = 3
+SDK_OPT_CHECK_BLOCKS_PER_CU = 4
 
 SDK_ORDER_MRV_UNIQUE = 0
 SDK_ORDER_LEX = 1

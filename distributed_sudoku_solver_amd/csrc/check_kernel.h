@@ -99,26 +99,37 @@ __device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int 
     return verdict;
 }
 
+// Full tiles are software-pipelined: the 6 dwordx4 loads of tile i+1 are issued
+// into registers before tile i is validated out of LDS, so every thread keeps
+// 96 B of HBM reads in flight across its compute phase.
 __global__ __launch_bounds__(kCheckThreads) void check_kernel(const uint8_t* __restrict__ boards,
                                                               uint8_t* __restrict__ verdict, uint64_t n) {
     // +16 B: the last thread's 22nd dword read runs one dword past the tile.
     __shared__ __attribute__((aligned(16))) u32x4 tile[kCheckTileVec + 1];
+    constexpr int kFull = kCheckTileVec / kCheckThreads;   // 5 vectors per thread
+    constexpr int kRem = kCheckTileVec % kCheckThreads;    // + 16 threads load a 6th
     const int t = threadIdx.x;
+    const uint64_t nfull = n / kCheckThreads;              // full tiles
     const uint64_t ntiles = (n + kCheckThreads - 1) / kCheckThreads;
-    for (uint64_t tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
+    u32x4 pre[kFull + 1];
+    uint64_t tix = blockIdx.x;
+    auto load_tile = [&](uint64_t ti) {
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(boards + ti * kCheckTileBytes);
+#pragma unroll
+        for (int j = 0; j < kFull; ++j) pre[j] = __builtin_nontemporal_load(&s4[j * kCheckThreads + t]);
+        if (t < kRem) pre[kFull] = __builtin_nontemporal_load(&s4[kFull * kCheckThreads + t]);
+    };
+    if (tix < nfull) load_tile(tix);
+    for (; tix < ntiles; tix += gridDim.x) {
         const uint64_t base = tix * kCheckThreads;
         const uint64_t cnt = min((uint64_t)kCheckThreads, n - base);
-        const uint8_t* src = boards + base * 81;
         if (cnt == (uint64_t)kCheckThreads) {
-            const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
 #pragma unroll
-            for (int j = 0; j < kCheckTileVec / kCheckThreads; ++j)  // 5 full sweeps
-                tile[j * kCheckThreads + t] = __builtin_nontemporal_load(&s4[j * kCheckThreads + t]);
-            if (t < kCheckTileVec % kCheckThreads)                    // 16 remaining vectors
-                tile[(kCheckTileVec / kCheckThreads) * kCheckThreads + t] =
-                    __builtin_nontemporal_load(&s4[(kCheckTileVec / kCheckThreads) * kCheckThreads + t]);
+            for (int j = 0; j < kFull; ++j) tile[j * kCheckThreads + t] = pre[j];
+            if (t < kRem) tile[kFull * kCheckThreads + t] = pre[kFull];
         } else {
             // ragged last tile: each thread copies its own record byte by byte
+            const uint8_t* src = boards + base * 81;
             uint8_t* tb = reinterpret_cast<uint8_t*>(tile);
             if ((uint64_t)t < cnt) {
 #pragma unroll
@@ -126,6 +137,8 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel(const uint8_t* __r
             }
         }
         __syncthreads();
+        const uint64_t nxt = tix + gridDim.x;
+        if (nxt < nfull) load_tile(nxt);                   // in flight during validation
         if ((uint64_t)t < cnt)
             verdict[base + t] = check_board_lds(reinterpret_cast<const uint32_t*>(tile), t);
         __syncthreads();

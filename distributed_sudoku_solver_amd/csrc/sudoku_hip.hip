@@ -57,6 +57,7 @@ struct sdk_ctx {
     int order = SDK_ORDER_MRV_UNIQUE;
     uint64_t budget = 0;
     int waves_per_cu = 16;
+    int check_blocks_per_cu = 3;
     // workspaces
     DevBuf stack, counter, in, mask, out, status, work, verdict;
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status;
@@ -95,7 +96,7 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
     if (n == 0) return SDK_OK;
     if (reinterpret_cast<uintptr_t>(d_in) & 15) return fail(SDK_EINVAL, "device boards must be 16-byte aligned");
     const uint64_t tiles = (n + sdk::kCheckThreads - 1) / sdk::kCheckThreads;
-    const unsigned grid = (unsigned)std::min<uint64_t>(tiles, (uint64_t)c->cus * 8);
+    const unsigned grid = (unsigned)std::min<uint64_t>(tiles, (uint64_t)c->cus * c->check_blocks_per_cu);
     hipEvent_t stop;
     int rc = timer_begin(c, &stop);
     if (rc) return rc;
@@ -309,6 +310,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 1 || value > 32) return fail(SDK_EINVAL, "waves per CU must be 1..32");
             c->waves_per_cu = (int)value;
             return SDK_OK;
+        case SDK_OPT_CHECK_BLOCKS_PER_CU:
+            if (value < 1 || value > 16) return fail(SDK_EINVAL, "check blocks per CU must be 1..16");
+            c->check_blocks_per_cu = (int)value;
+            return SDK_OK;
         default:
             return fail(SDK_EINVAL, "unknown option %d", key);
     }
@@ -321,6 +326,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_ORDER: *value = c->order; return SDK_OK;
         case SDK_OPT_NODE_BUDGET: *value = (int64_t)c->budget; return SDK_OK;
         case SDK_OPT_WAVES_PER_CU: *value = c->waves_per_cu; return SDK_OK;
+        case SDK_OPT_CHECK_BLOCKS_PER_CU: *value = c->check_blocks_per_cu; return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }
 }

@@ -78,8 +78,9 @@ __global__ __launch_bounds__(64) void expand_kernel(ExpandArgs a) {
                     }
                 }
                 cell = ma ? (uint32_t)__builtin_ctzll(ma) : 64u + (uint32_t)__builtin_ctzll(mb);
-                const uint32_t src_s = cell < 64 ? sa : sb;
-                m = (uint32_t)__builtin_amdgcn_readlane((int)src_s, (int)(cell & 63)) & kCands;
+                const uint32_t mA = (uint32_t)__builtin_amdgcn_readlane((int)sa, (int)(cell & 63));
+                const uint32_t mB = (uint32_t)__builtin_amdgcn_readlane((int)sb, (int)(cell & 63));
+                m = (cell < 64 ? mA : mB) & kCands;
                 nch = (uint32_t)__popc(m);
                 uint8_t* dst = a.prop + i * 81;
                 dst[lane] = (uint8_t)board_byte(inA, sa);

@@ -11,8 +11,9 @@
 // ignored (the reference never validates clues).
 //
 // Propagation round (all in LDS, no atomics):
-//   1. every lane writes its cell states to s_cell[81];
-//   2. lanes 0..26 each summarise one unit (row/col/box) from its 9 cells:
+//   1. every lane writes a bit-sliced contribution word per cell to s_cell[81];
+//   2. lanes 0..26 each summarise one unit (row/col/box) from its 9 words
+//      (two ops per cell: twos |= ones & w; ones |= w):
 //        T     = digits of single-candidate cells (givens and solved),
 //        once  = digits with exactly one candidate cell (hidden singles) -- only
 //                in "exact" units (no INERT cell, no duplicate given), where
@@ -36,7 +37,9 @@
 // in a per-workgroup HBM region (L2-resident in practice); branch records (cell,
 // untried digits) live in LDS.
 //
-// Boards are handed out to persistent wavefronts CHUNK at a time by one atomic.
+// Boards are handed out to persistent wavefronts `chunk` at a time by one atomic
+// (one returning atomic on one word saturates near 88 dequeues/us on MI355X, so
+// the host sizes the chunk to keep dequeues well below that).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -48,7 +51,7 @@ constexpr uint32_t kClue = 0x200u;
 constexpr uint32_t kInert = 0x400u;
 constexpr uint32_t kFixed = kClue | kInert;
 constexpr int kMaxDepth = 81;
-constexpr uint32_t kChunk = 4;
+constexpr uint32_t kChunk = 4;        // expand_kernel chunk; solve_kernel takes SolveArgs::chunk
 constexpr int kStackWordsPerBlock = kMaxDepth * 64;
 
 enum { P_CONTRA = 0, P_SOLVED = 1, P_OPEN = 2 };
@@ -69,6 +72,7 @@ struct SolveArgs {
     unsigned long long* count; // count mode: running total over the batch (atomic)
     unsigned long long* counts;// count mode: per-board counts (nullable)
     int count_mode;
+    uint32_t chunk;            // boards per dequeue (one atomic on `next` per chunk)
 };
 
 __device__ __forceinline__ uint32_t cell_init(uint32_t v) {
@@ -110,38 +114,42 @@ __device__ __forceinline__ void update_cell(uint32_t& x, uint32_t u, bool& bad, 
     }
 }
 
+// A cell's contribution to its units, as bit-sliced fields so that a unit is
+// summarised with two ops per cell (twos |= ones & w; ones |= w):
+//   [0..8]   candidates                 -> hidden singles / lost digits
+//   [9..17]  digit of a given           -> duplicate givens make a unit non-exact
+//   [18..26] digit of a solved non-given -> duplicates are a conflict
+//   [27]     out-of-domain given        -> unit non-exact
+__device__ __forceinline__ uint32_t contrib(uint32_t x) {
+    const uint32_t v = x & kCands;
+    if (x & kInert) return 1u << 27;
+    if (x & kClue) return v | (v << 9);
+    return is_single(v) ? (v | (v << 18)) : v;
+}
+
 __device__ __forceinline__ int propagate(const Wave& w, uint32_t& sa, uint32_t& sb) {
     for (;;) {
-        w.s_cell[w.lane] = sa;
-        if (w.hasB) w.s_cell[64 + w.lane] = sb;
+        w.s_cell[w.lane] = contrib(sa);
+        if (w.hasB) w.s_cell[64 + w.lane] = contrib(sb);
         __syncthreads();
         uint32_t summ = 0;
         if (w.lane < 27) {
-            uint32_t ones = 0, twos = 0, tn1 = 0, tn2 = 0, tc1 = 0, tc2 = 0, t = 0, inert = 0;
+            uint32_t ones = 0, twos = 0;
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
                 const uint32_t x = w.s_cell[w.ucell[k]];
-                const uint32_t v = x & kCands;
-                const uint32_t sv = is_single(v) ? v : 0u;
-                t |= sv;
-                twos |= ones & v;
-                ones |= v;
-                const bool clue = (x & kClue) != 0;
-                const uint32_t cv = clue ? v : 0u;
-                tc2 |= tc1 & cv;
-                tc1 |= cv;
-                const uint32_t nv = clue ? 0u : sv;
-                tn2 |= tn1 & nv;
-                tn1 |= nv;
-                inert |= x & kInert;
+                twos |= ones & x;
+                ones |= x;
             }
+            const uint32_t tc1 = (ones >> 9) & kCands, tc2 = (twos >> 9) & kCands;
+            const uint32_t tn1 = (ones >> 18) & kCands, tn2 = (twos >> 18) & kCands;
             bool conflict = (tn2 | (tn1 & tc1)) != 0;
             uint32_t once = 0;
-            if (!inert && !tc2) {
-                if (ones != kCands) conflict = true;
-                once = ones & ~twos;
+            if (!(ones >> 27) && !tc2) {           // exact unit: every digit exactly once
+                if ((ones & kCands) != kCands) conflict = true;
+                once = ones & ~twos & kCands;
             }
-            summ = t | (once << 16) | (conflict ? 0x80000000u : 0u);
+            summ = tc1 | tn1 | (once << 16) | (conflict ? 0x80000000u : 0u);
             w.s_unit[w.lane] = summ;
         }
         if (__any((int)(summ >> 31))) return P_CONTRA;
@@ -170,18 +178,19 @@ __device__ __forceinline__ void write_board(const Wave& w, uint8_t* dst, uint32_
     if (w.hasB) dst[64 + w.lane] = (uint8_t)b;
 }
 
+// Branch-free on purpose: two guarded stores to sa / sb get merged by the
+// compiler into one store through a phi of their addresses, which demotes both
+// to scratch memory.
 __device__ __forceinline__ void set_cell(const Wave& w, uint32_t& sa, uint32_t& sb, int cell, uint32_t d) {
-    if (cell < 64) {
-        if (w.lane == cell) sa = d;
-    } else {
-        if (w.lane == cell - 64) sb = d;
-    }
+    const bool mine = w.lane == (cell & 63);
+    sa = (mine && cell < 64) ? d : sa;
+    sb = (mine && cell >= 64) ? d : sb;
 }
 
 // Returns the number of completions found (stopping at `limit`, 0 = no limit),
 // or -1 when the node budget ran out.  The first completion is written to
 // `sol` when non-null.
-__device__ int64_t search(const Wave& w, int order, uint32_t sa0, uint32_t sb0, uint64_t limit,
+__device__ __forceinline__ int64_t search(const Wave& w, int order, uint32_t sa0, uint32_t sb0, uint64_t limit,
                           uint64_t budget, uint64_t& nodes, uint8_t* sol, uint32_t inA, uint32_t inB) {
     uint32_t sa = sa0, sb = sb0;
     int depth = 0;
@@ -212,8 +221,11 @@ __device__ int64_t search(const Wave& w, int order, uint32_t sa0, uint32_t sb0, 
                 }
             }
             const int cell = ma ? (int)__builtin_ctzll(ma) : 64 + (int)__builtin_ctzll(mb);
-            const uint32_t src = cell < 64 ? sa : sb;
-            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)src, cell & 63) & kCands;
+            // read both halves (a select of the two values would make the compiler take
+            // their addresses and demote sa/sb to scratch)
+            const uint32_t mA = (uint32_t)__builtin_amdgcn_readlane((int)sa, cell & 63);
+            const uint32_t mB = (uint32_t)__builtin_amdgcn_readlane((int)sb, cell & 63);
+            const uint32_t m = (cell < 64 ? mA : mB) & kCands;
             const uint32_t d = m & (0u - m);
             w.stk[depth * 64 + w.lane] = sa | (sb << 16);
             if (w.lane == 0) w.s_br[depth] = (uint32_t)cell | ((m ^ d) << 16);
@@ -280,10 +292,10 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     const int lane = w.lane;
     for (;;) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.next, kChunk);
+        if (lane == 0) base = atomicAdd(a.next, a.chunk);
         base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
         if ((uint64_t)base >= a.n) break;
-        const uint64_t end = min((uint64_t)base + kChunk, a.n);
+        const uint64_t end = min((uint64_t)base + a.chunk, a.n);
         for (uint64_t i = base; i < end; ++i) {
             const uint8_t* src = a.in + i * 81;
             const uint32_t inA = src[lane];
@@ -302,35 +314,28 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
             uint8_t* dst = a.out ? a.out + i * 81 : nullptr;
             uint64_t nodes = 0;
             int8_t st;
-            if (a.count_mode) {
-                // whole-subtree count (order-independent, so MRV); the batch stops
-                // early once the running total reaches the limit
-                int64_t c = 0;
-                bool skip = false;
-                if (a.limit) {
-                    unsigned long long tot = 0;
-                    if (lane == 0) tot = __hip_atomic_load(a.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    tot = __shfl(tot, 0);
-                    skip = tot >= a.limit;
-                }
-                if (!skip) c = search(w, ORDER_MRV, sa, sb, a.limit, a.budget, nodes, a.out ? dst : nullptr, inA, inB);
-                if (lane == 0) {
-                    if (c > 0) atomicAdd(a.count, (unsigned long long)c);
-                    if (a.counts) a.counts[i] = (unsigned long long)(c < 0 ? 0 : c);
-                }
-                st = c < 0 ? (int8_t)-2 : (c > 0 ? (int8_t)1 : (int8_t)0);
-                if (a.out && c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
-            } else {
-                int64_t c;
-                if (a.order == ORDER_LEX) {
-                    c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, dst, inA, inB);
-                } else {
-                    c = search(w, ORDER_MRV, sa, sb, 2, a.budget, nodes, dst, inA, inB);
-                    if (c >= 2) c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, dst, inA, inB);
-                }
-                st = c < 0 ? (int8_t)-2 : (c > 0 ? (int8_t)1 : (int8_t)0);
-                if (c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
+            // count mode: whole-subtree count (order-independent, so MRV); the
+            // batch stops early once the running total reaches the limit.
+            // solve mode: MRV search for <= 2 completions, or LEX for the first.
+            bool skip = false;
+            if (a.count_mode && a.limit) {
+                unsigned long long tot = 0;
+                if (lane == 0) tot = __hip_atomic_load(a.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                tot = __shfl(tot, 0);
+                skip = tot >= a.limit;
             }
+            const int order0 = (a.count_mode || a.order != ORDER_LEX) ? ORDER_MRV : ORDER_LEX;
+            const uint64_t lim0 = a.count_mode ? a.limit : (order0 == ORDER_LEX ? 1u : 2u);
+            int64_t c = 0;
+            if (!skip) c = search(w, order0, sa, sb, lim0, a.budget, nodes, dst, inA, inB);
+            if (!a.count_mode && order0 == ORDER_MRV && c >= 2)
+                c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, dst, inA, inB);
+            if (a.count_mode && lane == 0) {
+                if (c > 0) atomicAdd(a.count, (unsigned long long)c);
+                if (a.counts) a.counts[i] = (unsigned long long)(c < 0 ? 0 : c);
+            }
+            st = c < 0 ? (int8_t)-2 : (c > 0 ? (int8_t)1 : (int8_t)0);
+            if (dst && c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
             if (lane == 0) {
                 if (a.status) a.status[i] = st;
                 if (a.work) a.work[i] = nodes;

@@ -56,7 +56,7 @@ struct sdk_ctx {
     // options
     int order = SDK_ORDER_MRV_UNIQUE;
     uint64_t budget = 0;
-    int waves_per_cu = 16;
+    int waves_per_cu = 32;
     int check_blocks_per_cu = 3;
     // workspaces
     DevBuf stack, counter, in, mask, out, status, work, verdict;
@@ -111,8 +111,12 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
                  unsigned long long* d_counts = nullptr) {
     if (n == 0) return SDK_OK;
     if (n > 0x7FFFFFFFull) return fail(SDK_EINVAL, "at most 2^31-1 boards per call");
-    const uint64_t want = (n + sdk::kChunk - 1) / sdk::kChunk;
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->cus * c->waves_per_cu));
+    const uint64_t slots = (uint64_t)c->cus * c->waves_per_cu;
+    // ~16 dequeues per wave over the launch, 1..64 boards each; count mode uses
+    // single boards (subtrees differ by orders of magnitude)
+    const uint32_t chunk = count_mode ? 1u : (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, n / (slots * 16)));
+    const uint64_t want = (n + chunk - 1) / chunk;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, slots));
     int rc = ensure(c->stack, (size_t)grid * sdk::kStackWordsPerBlock * sizeof(uint32_t));
     if (rc) return rc;
     rc = ensure(c->counter, 256);
@@ -133,6 +137,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.count = d_count;
     a.counts = d_counts;
     a.count_mode = count_mode;
+    a.chunk = chunk;
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
     if (rc) return rc;

@@ -60,7 +60,7 @@ extern "C" {
 /* options for sdk_set_option */
 #define SDK_OPT_ORDER        1  /* SDK_ORDER_*                                        */
 #define SDK_OPT_NODE_BUDGET  2  /* max search nodes per board, 0 = unlimited          */
-#define SDK_OPT_WAVES_PER_CU 3  /* solver residency, 1..32 (default 16)               */
+#define SDK_OPT_WAVES_PER_CU 3  /* solver residency, 1..32 (default 32)               */
 #define SDK_OPT_CHECK_BLOCKS_PER_CU 4 /* checker grid = CUs x this, 1..16 (default 3)  */
 
 #define SDK_ORDER_MRV_UNIQUE 0  /* MRV search for <=2 solutions; lex re-search if >=2 */

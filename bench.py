@@ -43,6 +43,7 @@ def parse_args():
     ap.add_argument("--waves-per-cu", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--http-requests", type=int, default=20, help="C1 POST /solve leg (rank 0, N=1; 0 = skip)")
     ap.add_argument("--seed", type=int, default=20250614)
     return ap.parse_args()
 
@@ -107,6 +108,36 @@ def cpu_baseline(puzzles, seconds, threads):
                    f"restates DHT_Node.py:474-538, validations-exact), {threads} threads, "
                    f"{wall:.1f} s wall, {timeouts} hit the 2e9-validation budget"),
     }
+
+
+def http_leg(requests):
+    """Config C1: one puzzle POSTed to a single node's /solve (wiki 30-clue puzzle), end to end
+    over loopback HTTP, on a GPU-backed node (distributed_sudoku_solver_amd.node)."""
+    import urllib.request
+    from distributed_sudoku_solver_amd import synth
+    from distributed_sudoku_solver_amd.engine import SudokuEngine
+    from distributed_sudoku_solver_amd.node import SudokuNode
+    eng = SudokuEngine(0)
+    node = SudokuNode("127.0.0.1", 0, 0, engine=eng, delay_ms=0).start()
+    grid = [[int(c) for c in synth.WIKI[9 * r: 9 * r + 9]] for r in range(9)]
+    body = json.dumps({"sudoku": grid}).encode()
+    lat, ok = [], True
+    try:
+        for _ in range(requests + 2):
+            req = urllib.request.Request(f"http://127.0.0.1:{node.http_port}/solve", data=body, method="POST")
+            t0 = time.perf_counter()
+            with urllib.request.urlopen(req, timeout=60) as r:
+                out = json.loads(r.read())
+            lat.append(time.perf_counter() - t0)
+            ok &= "".join(str(v) for row in out["solution"] for v in row) == synth.WIKI_SOLUTION
+    finally:
+        node.stop(graceful=False)
+        eng.close()
+    lat = sorted(lat[2:])
+    return {"workload": "C1: wiki 30-clue puzzle POSTed to /solve on one node (loopback HTTP)",
+            "median_ms": 1000 * lat[len(lat) // 2], "min_ms": 1000 * lat[0], "requests": len(lat),
+            "solution_ok": bool(ok), "reference_ms": 87.0,
+            "reference_note": "DHT_Node.py single node, -d 0, measured in the build container (SURVEY §3.1)"}
 
 
 def main():
@@ -240,6 +271,9 @@ def main():
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         result["cpu_baseline"] = cpu_baseline(puzzles, args.cpu_seconds, threads)
+
+    if d.rank == 0 and d.world == 1 and args.http_requests > 0:
+        result["post_solve_latency"] = http_leg(args.http_requests)
 
     eng.close()
     if d.rank == 0:

@@ -1,0 +1,550 @@
+"""GPU-backed Sudoku node speaking the reference's HTTP and UDP protocol.
+
+Wire compatibility with DHT_Node.py (protocolo.pdf):
+  * UDP datagrams are pickled dicts with a 'method' key, the same 14 methods and
+    fields as DHT_Node.py:221-416 (TASK carries 'sudoku', 'range', 'uuid' and,
+    from an HTTP front end, 'initial_node').  Incoming datagrams go through a
+    restricted unpickler that only admits the builtins and uuid.UUID the
+    protocol uses (the reference's bare pickle.loads executes arbitrary code).
+  * HTTP: POST /solve -> 201 {"solution": grid, "duration": s};
+    GET /stats -> {"all": {"solved", "validations"}, "nodes": [...]} with the
+    reference's "validation" key for remote entries (DHT_Node.py:591);
+    GET /network -> {str(node): [str(pred), str(succ)]} (indent=4).
+  * Ring membership, coordinator join, heartbeats to the predecessor, failure
+    repair by the coordinator and re-execution of delegated tasks follow
+    DHT_Node.py:52-62, 137-209, 260-330.
+
+What changes (GPU-first):
+  * TASKs are executed by a worker thread that drains the whole queue into ONE
+    sdk_solve_batch launch (the reference serialises them on the UDP thread,
+    DHT_Node.py:225-250); the UDP loop never blocks on a solve.
+  * POST /solve hands its task straight to the worker and waits on an event
+    instead of a 10-ms polling loop (DHT_Node.py:553-554).
+  * No `sleep(2)` after a solution (DHT_Node.py:354,467) and an unsolvable
+    puzzle answers 201 {"solution": null} instead of hanging.
+  * `-d/--delay` keeps its role as a slow-node knob: milliseconds per search
+    node spent by the engine (the reference sleeps per guess, DHT_Node.py:524).
+"""
+import argparse
+import io
+import json
+import pickle
+import queue
+import socket
+import threading
+import time
+import uuid as uuidlib
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+import numpy as np
+
+from .engine import encode_solve_grid, range_to_mask
+from . import _lib as L
+
+RECV_BYTES = 1024          # DHT_Node.py:82,94
+HEARTBEAT_S = 5.0          # DHT_Node.py:43
+STATS_WAIT_S = 1.0         # DHT_Node.py:571
+
+
+class _ProtocolUnpickler(pickle.Unpickler):
+    """Admits exactly the types the protocol's dicts contain."""
+
+    _ALLOWED = {("builtins", "range"), ("builtins", "tuple"), ("builtins", "list"), ("builtins", "dict"),
+                ("builtins", "set"), ("builtins", "frozenset"), ("uuid", "UUID"), ("uuid", "SafeUUID")}
+
+    def find_class(self, module, name):
+        if (module, name) in self._ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"refusing {module}.{name}")
+
+
+def decode_datagram(data):
+    return _ProtocolUnpickler(io.BytesIO(data)).load()
+
+
+def encode_datagram(msg):
+    return pickle.dumps(msg)
+
+
+def _addr(a):
+    return (a[0], int(a[1])) if a is not None else None
+
+
+class SudokuNode:
+    """One ring member.  `engine` is a SudokuEngine (or anything with solve_batch)."""
+
+    def __init__(self, host, p2p_port, http_port, anchor=None, engine=None, delay_ms=0.0,
+                 heartbeat_s=HEARTBEAT_S, stats_wait_s=STATS_WAIT_S, solve_timeout_s=600.0, log=False):
+        self.host = host
+        self.port = p2p_port
+        self.http_port = http_port
+        self.anchor = _addr(anchor)
+        self.me = (host, p2p_port)
+        self.delay_ms = float(delay_ms)
+        self.heartbeat_s = heartbeat_s
+        self.stats_wait_s = stats_wait_s
+        self.solve_timeout_s = solve_timeout_s
+        self.log = log
+        if engine is None:
+            from .solver import default_engine
+            engine = default_engine()
+        self.engine = engine
+        # ring state (guarded by self.lock)
+        self.lock = threading.RLock()
+        self.network = []
+        self.coordinator = None
+        self.predecessor = None
+        self.neighbor = None
+        self.neighborfree = False
+        self.inside = False
+        self.last_heartbeat = time.time()
+        # work state
+        self.tasks = queue.Queue()               # pending TASK dicts
+        self.neighbor_tasks = []                 # tasks handed to the neighbour (re-run on its failure)
+        self.busy = False
+        self.done_uuids = set()                  # uuids already solved somewhere in the ring
+        self.waiters = {}                        # uuid -> (Event, [solution])
+        self.validations = 0
+        self.solved_count = 0
+        self.stats_replies = {}
+        self.running = False
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        self.sock.bind((host, p2p_port))
+        self.sock.settimeout(0.2)
+        self.port = self.sock.getsockname()[1]
+        self.me = (host, self.port)
+        self.httpd = ThreadingHTTPServer((host, http_port), _Handler)
+        self.httpd.node = self
+        self.httpd.daemon_threads = True
+        self.http_port = self.httpd.server_address[1]
+        self._threads = []
+        self._work = threading.Condition()
+
+    # ------------------------------------------------------------------ utils
+    def _log(self, *a):
+        if self.log:
+            print(f"[node {self.port}]", *a, flush=True)
+
+    def send(self, msg, addr):
+        try:
+            self.sock.sendto(encode_datagram(msg), _addr(addr))
+        except OSError as e:
+            self._log("send failed", e)
+
+    # -------------------------------------------------------------- lifecycle
+    def start(self):
+        self.running = True
+        with self.lock:
+            if self.anchor:
+                self.send({"method": "JOIN_REQ", "requestor": self.me}, self.anchor)
+            else:
+                self.network = [self.me]
+                self.coordinator = self.predecessor = self.neighbor = self.me
+                self.inside = True
+        for target in (self._udp_loop, self._worker_loop, self._heartbeat_loop, self.httpd.serve_forever):
+            t = threading.Thread(target=target, daemon=True)
+            t.start()
+            self._threads.append(t)
+        return self
+
+    def wait_joined(self, timeout=5.0):
+        t0 = time.time()
+        while not self.inside and time.time() - t0 < timeout:
+            time.sleep(0.01)
+        return self.inside
+
+    def stop(self, graceful=True):
+        """Leave the ring: queued tasks go to the neighbour, the coordinator is told
+        (DHT_Node.py:137-156); graceful=False simulates a crash."""
+        if graceful and self.running:
+            with self.lock:
+                pending = self._drain_queue()
+                if self.neighbor and self.neighbor != self.me:
+                    for t in pending:
+                        self.send(t, self.neighbor)
+                if self.coordinator and self.coordinator != self.me:
+                    self.send({"method": "NODE_FAILED", "node": self.me}, self.coordinator)
+        self.running = False
+        with self._work:
+            self._work.notify_all()
+        self.httpd.shutdown()
+        self.httpd.server_close()
+        self.sock.close()
+
+    # ------------------------------------------------------------- UDP side
+    def _udp_loop(self):
+        while self.running:
+            try:
+                data, addr = self.sock.recvfrom(RECV_BYTES)
+            except socket.timeout:
+                continue
+            except OSError:
+                break
+            try:
+                msg = decode_datagram(data)
+            except Exception as e:  # malformed or refused datagram
+                self._log("dropped datagram:", e)
+                continue
+            if isinstance(msg, dict) and "method" in msg:
+                try:
+                    self.handle(msg, addr)
+                except Exception as e:
+                    self._log("handler error", msg.get("method"), e)
+
+    def handle(self, msg, addr):
+        fn = getattr(self, "_on_" + str(msg["method"]), None)
+        if fn is None:
+            return
+        fn(msg)
+
+    def _on_TASK(self, msg):
+        self.enqueue(msg)
+
+    def _on_NEEDWORK(self, msg):
+        with self.lock:
+            self.neighborfree = True
+        self._maybe_delegate()
+
+    def _on_HEARTBEAT(self, msg):
+        self.last_heartbeat = time.time()
+
+    def _on_SOMETHING(self, msg):
+        pass
+
+    def _on_STOP(self, msg):
+        threading.Thread(target=self.stop, daemon=True).start()
+
+    def _on_NODE_FAILED(self, msg):
+        self._node_failed(_addr(msg["node"]))
+
+    def _on_JOIN_REQ(self, msg):
+        joiner = _addr(msg["requestor"])
+        with self.lock:
+            if self.coordinator != self.me:
+                self.send(msg, self.coordinator)
+                return
+            if joiner not in self.network:
+                self.network.append(joiner)
+            net = list(self.network)
+            for node in net:
+                if node != self.me:
+                    self.send({"method": "UPDATE_NETWORK", "network": net, "coordinator": self.coordinator}, node)
+            # joiner is appended last: it follows net[-2] and precedes net[0]
+            self.send({"method": "UPDATE_PREDECESSOR", "predecessor": joiner}, net[0])
+            self.send({"method": "UPDATE_NEIGHBOR", "neighbor": joiner}, net[-2])
+            self.send({"method": "JOIN_RES", "predecessor": net[-2], "neighbor": net[0], "network": net,
+                       "coordinator": self.coordinator}, joiner)
+            if net[0] == self.me:
+                self.predecessor = joiner
+            if net[-2] == self.me:
+                self.neighbor = joiner
+                self.neighborfree = False
+                self.last_heartbeat = time.time()
+
+    def _on_JOIN_RES(self, msg):
+        with self.lock:
+            self.predecessor = _addr(msg["predecessor"])
+            self.neighbor = _addr(msg["neighbor"])
+            self.network = [_addr(a) for a in msg["network"]]
+            self.coordinator = _addr(msg["coordinator"])
+            self.inside = True
+            self.neighborfree = False
+            self.last_heartbeat = time.time()
+            idle = not self.busy and self.tasks.empty()
+        if idle and self.predecessor != self.me:
+            self.send({"method": "NEEDWORK"}, self.predecessor)
+
+    def _on_UPDATE_PREDECESSOR(self, msg):
+        with self.lock:
+            self.predecessor = _addr(msg["predecessor"])
+            idle = not self.busy and self.tasks.empty()
+        if idle and self.predecessor != self.me:
+            self.send({"method": "NEEDWORK"}, self.predecessor)
+
+    def _on_UPDATE_NEIGHBOR(self, msg):
+        with self.lock:
+            self.neighbor = _addr(msg["neighbor"])
+            self.neighborfree = False
+            self.last_heartbeat = time.time()
+
+    def _on_UPDATE_NETWORK(self, msg):
+        with self.lock:
+            self.network = [_addr(a) for a in msg["network"]]
+            self.coordinator = _addr(msg["coordinator"])
+
+    def _on_SOLUTION_FOUND(self, msg):
+        uid = msg.get("uuid")
+        with self.lock:
+            self.solved_count += 1
+            self.done_uuids.add(uid)
+            self._purge(uid)
+        self._wake(uid, msg.get("solution"))
+
+    def _on_STATS_REQ(self, msg):
+        with self.lock:
+            peers = [n for n in self.network if n != self.me]
+            v = self.validations
+        for node in peers:
+            self.send({"method": "STATS_RES", "validations": v, "address": self.me}, node)
+
+    def _on_STATS_RES(self, msg):
+        a = _addr(msg["address"])
+        with self.lock:
+            self.stats_replies[f"{a[0]}:{a[1]}"] = int(msg["validations"])
+
+    # ----------------------------------------------------- membership repair
+    def _heartbeat_loop(self):
+        while self.running:
+            with self.lock:
+                pred, nb = self.predecessor, self.neighbor
+            if pred and pred != self.me:
+                self.send({"method": "HEARTBEAT"}, pred)
+            else:
+                self.last_heartbeat = time.time()
+            if nb and nb != self.me and time.time() - self.last_heartbeat > 2 * self.heartbeat_s:
+                self.last_heartbeat = time.time()
+                self._node_failed(nb)
+            time.sleep(self.heartbeat_s / 4)
+
+    def _node_failed(self, dead):
+        with self.lock:
+            if self.coordinator == dead:
+                self.coordinator = self.me
+            if self.coordinator == self.me:
+                if dead in self.network and len(self.network) > 1:
+                    i = self.network.index(dead)
+                    before = self.network[(i - 1) % len(self.network)]
+                    after = self.network[(i + 1) % len(self.network)]
+                    self.network.remove(dead)
+                    if before == self.me:
+                        self.neighbor, self.neighborfree = after, False
+                        self.last_heartbeat = time.time()
+                    else:
+                        self.send({"method": "UPDATE_NEIGHBOR", "neighbor": after}, before)
+                    if after == self.me:
+                        self.predecessor = before
+                    else:
+                        self.send({"method": "UPDATE_PREDECESSOR", "predecessor": before}, after)
+                    for node in self.network:
+                        if node != self.me:
+                            self.send({"method": "UPDATE_NETWORK", "network": list(self.network),
+                                       "coordinator": self.coordinator}, node)
+            else:
+                self.send({"method": "NODE_FAILED", "node": dead}, self.coordinator)
+            # re-run whatever was delegated to the (possibly dead) neighbour
+            rerun, self.neighbor_tasks = self.neighbor_tasks, []
+        for t in rerun:
+            self.enqueue(t)
+
+    # --------------------------------------------------------- task execution
+    def enqueue(self, task):
+        self.tasks.put(task)
+        with self._work:
+            self._work.notify()
+
+    def _drain_queue(self):
+        out = []
+        while True:
+            try:
+                out.append(self.tasks.get_nowait())
+            except queue.Empty:
+                return out
+
+    def _purge(self, uid):
+        keep = [t for t in self._drain_queue() if t.get("uuid") != uid]
+        for t in keep:
+            self.tasks.put(t)
+        self.neighbor_tasks = [t for t in self.neighbor_tasks if t.get("uuid") != uid]
+
+    def _maybe_delegate(self):
+        """A free neighbour gets one queued task (DHT_Node.py:491-498)."""
+        with self.lock:
+            if not (self.neighborfree and self.neighbor and self.neighbor != self.me):
+                return
+            try:
+                t = self.tasks.get_nowait()
+            except queue.Empty:
+                return
+            self.neighborfree = False
+            self.neighbor_tasks.append(t)
+            self.send(t, self.neighbor)
+
+    def _worker_loop(self):
+        while self.running:
+            with self._work:
+                while self.running and self.tasks.empty():
+                    self._work.wait(0.5)
+            if not self.running:
+                return
+            with self.lock:
+                batch = [t for t in self._drain_queue() if t.get("uuid") not in self.done_uuids]
+                self.busy = True
+            if batch:
+                self._run_batch(batch)
+            with self.lock:
+                self.busy = False
+                pred = self.predecessor
+                idle = self.tasks.empty()
+            if idle and pred and pred != self.me:
+                self.send({"method": "NEEDWORK"}, pred)        # DHT_Node.py:245-248
+
+    def _run_batch(self, batch):
+        """All queued TASKs in one sdk_solve_batch launch."""
+        boards = np.stack([encode_solve_grid(t["sudoku"]) for t in batch])
+        masks = np.array([range_to_mask(t.get("range", range(1, 10))) for t in batch], dtype=np.uint16)
+        out, status, work = self.engine.solve_batch(boards, masks, want_work=True)
+        nodes = int(work.sum())
+        if self.delay_ms > 0:
+            time.sleep(self.delay_ms * nodes / 1000.0)
+        with self.lock:
+            self.validations += nodes
+        for t, o, st in zip(batch, out, status):
+            uid = t.get("uuid")
+            if st == L.SDK_SOLVED:
+                grid = [list(row) for row in t["sudoku"]]
+                for r in range(9):
+                    for c in range(9):
+                        if grid[r][c] == 0:
+                            grid[r][c] = int(o[9 * r + c])
+                self._solved(uid, grid)
+            elif st == L.SDK_BUDGET_HIT:
+                self._log("budget exhausted for", uid)
+            else:
+                # this task's digit range has no completion; when the task is the
+                # whole puzzle (HTTP origin) the answer is "no solution"
+                if t.get("initial_node") is not None and _is_full_range(t.get("range")):
+                    self._wake(uid, None)
+
+    def _solved(self, uid, grid):
+        with self.lock:
+            if uid in self.done_uuids:
+                return
+            self.done_uuids.add(uid)
+            self.solved_count += 1
+            self._purge(uid)
+            peers = [n for n in self.network if n != self.me]
+        for node in peers:
+            self.send({"method": "SOLUTION_FOUND", "solution": grid, "node": self.me, "uuid": uid}, node)
+        self._wake(uid, grid)
+
+    def _wake(self, uid, solution):
+        with self.lock:
+            w = self.waiters.get(uid)
+        if w is not None:
+            w[1].append(solution)
+            w[0].set()
+
+    # ------------------------------------------------------------- HTTP side
+    def solve_http(self, puzzle):
+        uid = uuidlib.uuid4()
+        ev = threading.Event()
+        box = []
+        with self.lock:
+            self.waiters[uid] = (ev, box)
+        self.enqueue({"method": "TASK", "sudoku": puzzle, "range": range(1, 10), "uuid": uid,
+                      "initial_node": self.me})
+        ok = ev.wait(self.solve_timeout_s)
+        with self.lock:
+            self.waiters.pop(uid, None)
+        if not ok:
+            raise TimeoutError("no solution reported in time")
+        return box[0] if box else None
+
+    def stats(self):
+        with self.lock:
+            peers = [n for n in self.network if n != self.me]
+            self.stats_replies = {}
+        for node in peers:
+            self.send({"method": "STATS_REQ"}, node)
+        t0 = time.time()
+        while peers and time.time() - t0 < self.stats_wait_s:
+            with self.lock:
+                if len(self.stats_replies) >= len(peers):
+                    break
+            time.sleep(0.005)
+        with self.lock:
+            replies = dict(self.stats_replies)
+            mine = int(self.validations)
+            solved = self.solved_count
+        nodes = [{"address": f"{self.host}:{self.port}", "validations": mine}]
+        nodes += [{"address": a, "validation": v} for a, v in replies.items()]   # reference key, DHT_Node.py:591
+        return {"all": {"solved": solved, "validations": mine + sum(replies.values())}, "nodes": nodes}
+
+    def network_view(self):
+        with self.lock:
+            net = list(self.network)
+        n = len(net)
+        return {str(a): [str(net[(i - 1) % n]), str(net[(i + 1) % n])] for i, a in enumerate(net)}
+
+
+def _is_full_range(r):
+    try:
+        return range_to_mask(r if r is not None else range(1, 10)) == 0x3FE
+    except ValueError:
+        return False
+
+
+class _Handler(BaseHTTPRequestHandler):
+    def log_message(self, *a):
+        pass
+
+    def _reply(self, code, obj, indent=None):
+        body = json.dumps(obj, indent=indent).encode()
+        self.send_response(code)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+
+    def do_POST(self):
+        node = self.server.node
+        if self.path != "/solve":
+            return self._reply(404, {"error": "not found"})
+        t0 = time.time()
+        try:
+            n = int(self.headers.get("Content-Length", 0))
+            puzzle = json.loads(self.rfile.read(n))["sudoku"]
+            if len(puzzle) != 9 or any(len(row) != 9 for row in puzzle):
+                raise ValueError("sudoku must be 9 rows of 9 cells")
+        except Exception as e:
+            return self._reply(400, {"error": str(e)})
+        try:
+            solution = node.solve_http(puzzle)
+        except TimeoutError as e:
+            return self._reply(504, {"error": str(e)})
+        self._reply(201, {"solution": solution, "duration": time.time() - t0})
+
+    def do_GET(self):
+        node = self.server.node
+        if self.path == "/stats":
+            return self._reply(200, node.stats())
+        if self.path == "/network":
+            return self._reply(200, node.network_view(), indent=4)
+        self._reply(404, {"error": "not found"})
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="GPU-backed distributed Sudoku solver node")
+    ap.add_argument("-p", "--port", type=int, required=True, help="HTTP port")
+    ap.add_argument("-s", "--p2p-port", type=int, required=True, help="UDP port")
+    ap.add_argument("-a", "--anchor", type=str, help="host:port of a ring member to join")
+    ap.add_argument("-d", "--delay", type=float, default=1.0, help="ms per engine search node (slow-node knob)")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--device", type=int, default=0)
+    args = ap.parse_args(argv)
+    anchor = None
+    if args.anchor:
+        h, p = args.anchor.rsplit(":", 1)
+        anchor = (h, int(p))
+    from .engine import SudokuEngine
+    node = SudokuNode(args.host, args.p2p_port, args.port, anchor, SudokuEngine(args.device), args.delay, log=True)
+    node.start()
+    try:
+        while True:
+            time.sleep(1)
+    except KeyboardInterrupt:
+        node.stop()
+
+
+if __name__ == "__main__":
+    main()

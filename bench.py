@@ -45,6 +45,9 @@ def parse_args():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--http-requests", type=int, default=20, help="C1 POST /solve leg (rank 0, N=1; 0 = skip)")
     ap.add_argument("--seed", type=int, default=20250614)
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
+                    help="per-launch HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this bench "
+                         "(tools/gpu_round.sh pmc); '' = report traffic null")
     return ap.parse_args()
 
 
@@ -83,6 +86,16 @@ class Dist:
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
+
+
+def pmc_traffic(path, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_summary.py:
+    2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f).get(kernel)
+    return None if rec is None else float(rec["traffic_bytes"])
 
 
 def cpu_baseline(puzzles, seconds, threads):
@@ -215,7 +228,9 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": None,
+            # the committed PMC passes ran this bench at its default sizes
+            "traffic": pmc_traffic(args.pmc_summary, "sdk::solve_kernel") if n == 10_000_000 else None,
+            "traffic_source": args.pmc_summary and os.path.relpath(args.pmc_summary, ROOT),
             "kernel": "sdk::solve_kernel",
             "avg_kernel_ms": avg_kernel_s * 1000.0,
             "note": "search is VALU/LDS-latency bound; HBM fraction reported per contract",
@@ -263,7 +278,10 @@ def main():
             "unit": "boards/s",
             "avg_kernel_ms": ck_s * 1000.0,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBPS, "traffic": None, "kernel": "sdk::check_kernel"},
+                         "frac": ach / HBM_PEAK_GBPS,
+                         "traffic": pmc_traffic(args.pmc_summary, "sdk::check_kernel")
+                         if nb == 100_000_000 else None,
+                         "kernel": "sdk::check_kernel"},
             "parity": {"mismatched_boards": cbad, "checked_boards": d.world * nb},
         }
 

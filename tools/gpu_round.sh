@@ -1,0 +1,42 @@
+#!/bin/bash
+# One GPU-box pass: gpu tests, smoke, bench, rocprof kernel stats, HBM PMC passes.
+# usage (from the repo root on the box): tools/gpu_round.sh <tag> [tests|bench|prof|pmc ...]
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+tag=${1:-r01}; shift
+steps=${*:-tests bench prof pmc}
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+root=$(pwd)
+
+for s in $steps; do
+  case $s in
+  tests)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      > "$out/pytest_gpu.log" 2>&1 || { echo "gpu tests failed"; tail -40 "$out/pytest_gpu.log"; exit 1; }
+    tail -3 "$out/pytest_gpu.log"
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
+      || { echo "smoke failed"; tail -20 "$out/smoke.log"; exit 1; }
+    cat "$out/smoke.log" ;;
+  bench)
+    timeout -k 10 420 python -u bench.py > "$out/bench.json" 2> "$out/bench.err" \
+      || { echo "bench failed"; tail -20 "$out/bench.err"; exit 1; }
+    cat "$out/bench.json" ;;
+  prof)
+    (cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats -d "$root/$out/prof" -o run \
+      --output-format csv -- python3 "$root/bench.py" --cpu-seconds 0 --http-requests 0 \
+      > "$root/$out/prof_bench.json" 2> "$root/$out/prof.err") \
+      || { echo "rocprof failed"; tail -20 "$out/prof.err"; exit 1; }
+    find "$out/prof" -name '*kernel_stats.csv' -exec cat {} \; ;;
+  pmc)
+    for c in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$root/$out/pmc_$c" -o run -- \
+        python3 "$root/bench.py" --steps 2 --warmup 0 --check-steps 2 --cpu-seconds 0 --http-requests 0 \
+        > "$root/$out/pmc_$c.json" 2> "$root/$out/pmc_$c.err") \
+        || { echo "pmc $c failed"; tail -20 "$out/pmc_$c.err"; exit 1; }
+    done
+    python3 tools/pmc_summary.py "$out" | tee "$out/pmc_summary.txt" ;;
+  *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

@@ -10,8 +10,11 @@ ranks time.  After timing, every solved board is compared with its expected
 solution (known by construction) -- a mismatch fails the run.
 
 Side legs on the same run: the batched checker (config C3, 100M boards per GPU
-by default, HBM-bound) and the CPU baseline (rank 0, N=1 only): the oracle's C
-port of the reference's naive DFS on a bounded sample of the same puzzles.
+by default, HBM-bound), config C2 (1M ~30-clue puzzles per GPU), config C5 (an
+exhaustive count of one 15-clue board, its frontier split over all ranks, the
+count combined by an RCCL all-reduce over xGMI), config C1 (POST /solve latency on
+a GPU-backed node) and the CPU baseline (rank 0, N=1 only): the oracle's C port of
+the reference's naive DFS on a bounded sample of the same puzzles.
 """
 import argparse
 import json
@@ -45,6 +48,11 @@ def parse_args():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--http-requests", type=int, default=20, help="C1 POST /solve leg (rank 0, N=1; 0 = skip)")
     ap.add_argument("--seed", type=int, default=20250614)
+    ap.add_argument("--c2-puzzles", type=int, default=1_000_000,
+                    help="C2 leg: ~30-clue unique puzzles per GPU (0 = skip)")
+    ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
+    ap.add_argument("--leg-timeout", type=float, default=120.0,
+                    help="watchdog for the side legs: print what was measured and exit")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
                     help="per-launch HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this bench "
                          "(tools/gpu_round.sh pmc); '' = report traffic null")
@@ -121,6 +129,71 @@ def cpu_baseline(puzzles, seconds, threads):
                    f"restates DHT_Node.py:474-538, validations-exact), {threads} threads, "
                    f"{wall:.1f} s wall, {timeouts} hit the 2e9-validation budget"),
     }
+
+
+def c2_leg(eng, d, args, synth):
+    """Config C2: ~30-clue unique puzzles, resident in HBM, one launch per step."""
+    n = args.c2_puzzles
+    p, sol = synth.make_30clue(n, seed=args.seed + 31 + 1000 * d.rank)
+    d_in, d_out, d_st = eng.alloc(n * 81), eng.alloc(n * 81), eng.alloc(n)
+    d_in.upload(p)
+    eng.solve_batch_dev(d_in, d_out, d_st, n)
+    eng.synchronize()
+    eng.timer_reset()
+    d.barrier()
+    t0 = time.perf_counter()
+    steps = 5
+    for _ in range(steps):
+        eng.solve_batch_dev(d_in, d_out, d_st, n)
+    eng.synchronize()
+    d.barrier()
+    el = d.max(time.perf_counter() - t0)
+    ms, nl = eng.timer_read()
+    out = np.empty((n, 81), np.uint8)
+    st = np.empty(n, np.int8)
+    d_out.download(out)
+    d_st.download(st)
+    bad = int(d.sum(int(((out != sol).any(axis=1) | (st != 1)).sum())))
+    for b in (d_in, d_out, d_st):
+        b.free()
+    k_s = ms / 1000.0 / max(nl, 1)
+    leg = {"workload": f"C2: {n} ~30-clue unique puzzles per GPU (seeds S1-S5 solutions + 13 cells, symmetries)",
+           "value": d.world * n * steps / el, "unit": "puzzles/s", "avg_kernel_ms": k_s * 1000.0,
+           "roofline": {"bound": "hbm", "achieved": SOLVE_BYTES_PER_PUZZLE * n / k_s / 1e9, "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": SOLVE_BYTES_PER_PUZZLE * n / k_s / 1e9 / HBM_PEAK_GBPS,
+                        "kernel": "sdk::solve_kernel"},
+           "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
+    if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
+        leg["cpu_baseline"] = cpu_baseline(p, min(5.0, args.cpu_seconds),
+                                           max(1, min(args.cpu_threads, os.cpu_count() or 1)))
+    return leg
+
+
+C5_BOARD_SOLUTIONS = 3_481_026    # SURVEY §8(d) C5: S1 with its last row cleared (15 clues)
+
+
+def c5_leg(eng, d, synth):
+    """Config C5: exhaustive count of one 15-clue board.  Every rank expands the same frontier
+    and counts its interleaved share; one RCCL all-reduce (device memory, xGMI) combines them."""
+    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count
+    board = synth.parse(synth.SEEDS17["S1"][:-9] + "0" * 9)
+    comm = RcclComm(eng, d.rank, d.world) if d.world > 1 else None
+    try:
+        sharded_count(eng, board, d.rank, d.world, comm=comm)            # warm-up
+        walls = []
+        for _ in range(3):
+            d.barrier()
+            t0 = time.perf_counter()
+            total, st, size = sharded_count(eng, board, d.rank, d.world, comm=comm)
+            walls.append(d.max(time.perf_counter() - t0))
+    finally:
+        if comm is not None:
+            comm.close()
+    w = min(walls)
+    return {"workload": "C5: count every completion of S1 minus its last row (15 clues), frontier split over "
+                        f"{d.world} GPU(s)" + (", RCCL all-reduce" if d.world > 1 else ""),
+            "solutions": total, "expected": C5_BOARD_SOLUTIONS, "ok": total == C5_BOARD_SOLUTIONS and st == 1,
+            "frontier_boards": size, "wall_ms": w * 1000.0, "value": total / w, "unit": "solutions/s"}
 
 
 def http_leg(requests):
@@ -285,6 +358,27 @@ def main():
             "parity": {"mismatched_boards": cbad, "checked_boards": d.world * nb},
         }
 
+    # side legs run under a watchdog: if one stalls (e.g. a collective), rank 0
+    # still prints the line with everything measured so far
+    import threading
+
+    def _watchdog():
+        if d.rank == 0:
+            result["watchdog"] = f"side legs stopped after {args.leg_timeout} s"
+            print(json.dumps(result), flush=True)
+        os._exit(3 if bad_total else 0)
+    dog = threading.Timer(args.leg_timeout, _watchdog)
+    dog.daemon = True
+    dog.start()
+
+    # ------------------------------------------------------------ C2 leg
+    if args.c2_puzzles > 0:
+        result["c2_30clue"] = c2_leg(eng, d, args, synth)
+
+    # ------------------------------------------------------------ C5 leg
+    if args.count_leg:
+        result["c5_count"] = c5_leg(eng, d, synth)
+
     # ---------------------------------------------------------- CPU baseline
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -293,6 +387,7 @@ def main():
     if d.rank == 0 and d.world == 1 and args.http_requests > 0:
         result["post_solve_latency"] = http_leg(args.http_requests)
 
+    dog.cancel()
     eng.close()
     if d.rank == 0:
         print(json.dumps(result), flush=True)

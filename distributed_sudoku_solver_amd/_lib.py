@@ -15,6 +15,7 @@ SDK_OK = 0
 SDK_EINVAL = -1
 SDK_EHIP = -2
 SDK_ENOMEM = -3
+SDK_ECOMM = -4
 
 SDK_SOLVED = 1
 SDK_UNSOLVABLE = 0
@@ -27,9 +28,25 @@ SDK_OPT_ORDER = 1
 SDK_OPT_NODE_BUDGET = 2
 SDK_OPT_WAVES_PER_CU = 3
 SDK_OPT_CHECK_BLOCKS_PER_CU = 4
+SDK_OPT_WORK_COUNTER = 5
+SDK_OPT_DEVICE_CUS = 6
+
+SDK_WORK_NODES = 0
+SDK_WORK_ROUNDS = 1
 
 SDK_ORDER_MRV_UNIQUE = 0
 SDK_ORDER_LEX = 1
+
+SDK_FRONTIER_COUNT = 0
+SDK_FRONTIER_FIRST = 1
+
+SDK_COMM_ID_BYTES = 128
+SDK_COMM_U64 = 0
+SDK_COMM_I64 = 1
+SDK_COMM_U8 = 2
+SDK_COMM_SUM = 0
+SDK_COMM_MIN = 1
+SDK_COMM_MAX = 2
 
 # every symbol the header declares: name -> (restype, argtypes)
 _vp = ctypes.c_void_p
@@ -49,6 +66,16 @@ SIGNATURES = {
     "sdk_count_solutions_slice": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                                  ctypes.POINTER(ctypes.c_int8)]),
+    "sdk_frontier_build": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64,
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "sdk_frontier_count_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_uint64, _vp]),
+    "sdk_frontier_first_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]),
+    "sdk_comm_unique_id": (ctypes.c_int, [_vp]),
+    "sdk_comm_init": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
+    "sdk_comm_destroy": (ctypes.c_int, [_vp]),
+    "sdk_comm_allreduce_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int, ctypes.c_int]),
+    "sdk_comm_broadcast_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int]),
     "sdk_dev_alloc": (ctypes.c_int, [_vp, _sz, ctypes.POINTER(_vp)]),
     "sdk_dev_free": (ctypes.c_int, [_vp, _vp]),
     "sdk_memcpy_h2d": (ctypes.c_int, [_vp, _vp, _vp, _sz]),

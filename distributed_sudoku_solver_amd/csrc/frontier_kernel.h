@@ -15,6 +15,16 @@
 //   emit_kernel    one wave per parent writes its children contiguously at
 //                  offset[parent], digits ascending: children of one parent
 //                  and parents in order -> a coalesced, ordered HBM array.
+//   first_hit_kernel  after a batched solve of frontier boards [lo, hi): the
+//                  lowest index whose status is not "no solution" and its board.
+//
+// First-solution mode (keep_leaves): a board that propagates to SOLVED stays in
+// the frontier as its own single child instead of being counted, and the branch
+// cell is the lowest-index open cell (ORDER_LEX) with children in ascending digit
+// order.  Every cell before the branch cell is forced, so the frontier in index
+// order is sorted by the completions below each board: the reference's lex-first
+// solution (DHT_Node.py:474-538) is the lex-first completion of the lowest-index
+// frontier board that has one.
 #pragma once
 #include "solve_kernel.h"
 
@@ -28,9 +38,14 @@ struct ExpandArgs {
     uint16_t* bmask;          // [m] branch candidates (bit d-1 = digit d)
     uint32_t* nchild;         // [m]
     unsigned long long* leaves;
+    unsigned long long* open;  // boards that branched at this level
     uint32_t* next;
     int order;
+    const uint16_t* mask;      // nullable, level 0 only: first-cell digit mask of board 0
+    int keep_leaves;           // first-solution mode (see header)
 };
+
+constexpr uint16_t kKeepBoard = 0x8000;   // bmask flag: emit the propagated board itself
 
 __device__ __forceinline__ uint32_t board_byte(uint32_t in, uint32_t s) {
     // givens keep their byte; single-valued cells become givens; open cells stay 0
@@ -58,11 +73,32 @@ __global__ __launch_bounds__(64) void expand_kernel(ExpandArgs a) {
             const uint32_t inB = w.hasB ? (uint32_t)src[64 + lane] : 0u;
             uint32_t sa = cell_init(inA);
             uint32_t sb = w.hasB ? cell_init(inB) : kInert;
-            const int r = propagate(w, sa, sb);
+            if (a.mask) {
+                // TASK `range` on the lowest-index empty input cell (DHT_Node.py:474,522,531)
+                const uint32_t fm = ((uint32_t)a.mask[i] >> 1) & kCands;
+                const unsigned long long za = __ballot(inA == 0);
+                const unsigned long long zb = __ballot(w.hasB && inB == 0);
+                if (za) {
+                    if (lane == (int)__builtin_ctzll(za)) sa &= fm | ~kCands;
+                } else if (zb) {
+                    if (lane == (int)__builtin_ctzll(zb)) sb &= fm | ~kCands;
+                }
+            }
+            uint64_t rounds = 0;
+            const int r = propagate(w, sa, sb, rounds);
             uint32_t nch = 0, cell = 0, m = 0;
             if (r == P_SOLVED) {
-                if (lane == 0) atomicAdd(a.leaves, 1ull);
+                if (a.keep_leaves) {
+                    nch = 1;
+                    m = kKeepBoard;
+                    uint8_t* dst = a.prop + i * 81;
+                    dst[lane] = (uint8_t)board_byte(inA, sa);
+                    if (w.hasB) dst[64 + lane] = (uint8_t)board_byte(inB, sb);
+                } else if (lane == 0) {
+                    atomicAdd(a.leaves, 1ull);
+                }
             } else if (r == P_OPEN) {
+                if (lane == 0) atomicAdd(a.open, 1ull);
                 const uint32_t pa = open_count(sa);
                 const uint32_t pb = w.hasB ? open_count(sb) : 0u;
                 unsigned long long ma, mb;
@@ -133,10 +169,16 @@ __global__ __launch_bounds__(64) void emit_kernel(const uint8_t* __restrict__ pr
     for (uint64_t i = blockIdx.x; i < m; i += gridDim.x) {
         uint32_t mask = bmask[i];
         if (!mask) continue;
-        const uint32_t cell = bcell[i];
         const uint32_t a = prop[i * 81 + lane];
         const uint32_t b = hasB ? prop[i * 81 + 64 + lane] : 0u;
         uint64_t j = off[i];
+        if (mask & kKeepBoard) {   // solved leaf kept in place (first-solution mode)
+            uint8_t* dst = out + j * 81;
+            dst[lane] = (uint8_t)a;
+            if (hasB) dst[64 + lane] = (uint8_t)b;
+            continue;
+        }
+        const uint32_t cell = bcell[i];
         while (mask) {
             const uint32_t d = (uint32_t)__ffs(mask);  // digit
             mask &= mask - 1;
@@ -145,6 +187,49 @@ __global__ __launch_bounds__(64) void emit_kernel(const uint8_t* __restrict__ pr
             if (hasB) dst[64 + lane] = (uint8_t)((uint32_t)(64 + lane) == cell ? d : b);
             ++j;
         }
+    }
+}
+
+// status[0..n) of frontier boards lo .. lo+n-1 (dense).  found <- lo + the first i
+// whose status is not 0 (solved, or budget hit: either ends a lex-ordered scan),
+// INT64_MAX if none; best[0..80] <- that board's output, best[81] <- its status.
+__global__ __launch_bounds__(256) void first_hit_kernel(const int8_t* __restrict__ status,
+                                                        const uint8_t* __restrict__ out, uint64_t n, uint64_t lo,
+                                                        long long* found, uint8_t* best) {
+    __shared__ unsigned long long s_min[4];
+    const int t = threadIdx.x;
+    unsigned long long mine = ~0ull;
+    for (uint64_t i = t; i < n; i += 256)
+        if (status[i] != 0) { mine = i; break; }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mine = min(mine, (unsigned long long)__shfl_xor(mine, d));
+    if ((t & 63) == 0) s_min[t >> 6] = mine;
+    __syncthreads();
+    const unsigned long long first = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
+    if (first == ~0ull) {
+        if (t == 0) *found = 0x7FFFFFFFFFFFFFFFll;
+        return;
+    }
+    if (t < 81) best[t] = out[first * 81 + t];
+    if (t == 81) best[81] = (uint8_t)status[first];
+    if (t == 0) *found = (long long)(lo + first);
+}
+
+// d_result <- {*count, number of status == -2 (node budget hit)} for n count-mode boards.
+__global__ __launch_bounds__(256) void count_result_kernel(const int8_t* __restrict__ status, uint64_t n,
+                                                           const unsigned long long* count,
+                                                           unsigned long long* result) {
+    __shared__ unsigned long long s_hits[4];
+    const int t = threadIdx.x;
+    unsigned long long hits = 0;
+    for (uint64_t i = t; i < n; i += 256) hits += status[i] == -2;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) hits += __shfl_xor(hits, d);
+    if ((t & 63) == 0) s_hits[t >> 6] = hits;
+    __syncthreads();
+    if (t == 0) {
+        result[0] = *count;
+        result[1] = s_hits[0] + s_hits[1] + s_hits[2] + s_hits[3];
     }
 }
 

@@ -73,6 +73,9 @@ struct SolveArgs {
     unsigned long long* counts;// count mode: per-board counts (nullable)
     int count_mode;
     uint32_t chunk;            // boards per dequeue (one atomic on `next` per chunk)
+    int work_rounds;           // work[] counts propagation rounds instead of search nodes
+    uint64_t in_first;         // board i of the launch reads in[(in_first + i*in_step)*81];
+    uint64_t in_step;          // outputs stay dense (out[i*81], status[i]); 0/1 = contiguous
 };
 
 __device__ __forceinline__ uint32_t cell_init(uint32_t v) {
@@ -127,8 +130,9 @@ __device__ __forceinline__ uint32_t contrib(uint32_t x) {
     return is_single(v) ? (v | (v << 18)) : v;
 }
 
-__device__ __forceinline__ int propagate(const Wave& w, uint32_t& sa, uint32_t& sb) {
+__device__ __forceinline__ int propagate(const Wave& w, uint32_t& sa, uint32_t& sb, uint64_t& rounds) {
     for (;;) {
+        ++rounds;
         w.s_cell[w.lane] = contrib(sa);
         if (w.hasB) w.s_cell[64 + w.lane] = contrib(sb);
         __syncthreads();
@@ -191,12 +195,13 @@ __device__ __forceinline__ void set_cell(const Wave& w, uint32_t& sa, uint32_t& 
 // or -1 when the node budget ran out.  The first completion is written to
 // `sol` when non-null.
 __device__ __forceinline__ int64_t search(const Wave& w, int order, uint32_t sa0, uint32_t sb0, uint64_t limit,
-                          uint64_t budget, uint64_t& nodes, uint8_t* sol, uint32_t inA, uint32_t inB) {
+                          uint64_t budget, uint64_t& nodes, uint64_t& rounds, uint8_t* sol, uint32_t inA,
+                          uint32_t inB) {
     uint32_t sa = sa0, sb = sb0;
     int depth = 0;
     int64_t count = 0;
     for (;;) {
-        int r = propagate(w, sa, sb);
+        int r = propagate(w, sa, sb, rounds);
         ++nodes;
         if (budget && nodes > budget) return -1;
         if (r == P_SOLVED) {
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
         if ((uint64_t)base >= a.n) break;
         const uint64_t end = min((uint64_t)base + a.chunk, a.n);
         for (uint64_t i = base; i < end; ++i) {
-            const uint8_t* src = a.in + i * 81;
+            const uint8_t* src = a.in + (a.in_first + i * a.in_step) * 81;
             const uint32_t inA = src[lane];
             const uint32_t inB = w.hasB ? (uint32_t)src[64 + lane] : 0u;
             uint32_t sa = cell_init(inA);
@@ -312,7 +317,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
                 if (lane == (int)__builtin_ctzll(zb)) sb &= fm | ~kCands;
             }
             uint8_t* dst = a.out ? a.out + i * 81 : nullptr;
-            uint64_t nodes = 0;
+            uint64_t nodes = 0, rounds = 0;
             int8_t st;
             // count mode: whole-subtree count (order-independent, so MRV); the
             // batch stops early once the running total reaches the limit.
@@ -327,9 +332,9 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
             const int order0 = (a.count_mode || a.order != ORDER_LEX) ? ORDER_MRV : ORDER_LEX;
             const uint64_t lim0 = a.count_mode ? a.limit : (order0 == ORDER_LEX ? 1u : 2u);
             int64_t c = 0;
-            if (!skip) c = search(w, order0, sa, sb, lim0, a.budget, nodes, dst, inA, inB);
+            if (!skip) c = search(w, order0, sa, sb, lim0, a.budget, nodes, rounds, dst, inA, inB);
             if (!a.count_mode && order0 == ORDER_MRV && c >= 2)
-                c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, dst, inA, inB);
+                c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, rounds, dst, inA, inB);
             if (a.count_mode && lane == 0) {
                 if (c > 0) atomicAdd(a.count, (unsigned long long)c);
                 if (a.counts) a.counts[i] = (unsigned long long)(c < 0 ? 0 : c);
@@ -338,7 +343,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
             if (dst && c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
             if (lane == 0) {
                 if (a.status) a.status[i] = st;
-                if (a.work) a.work[i] = nodes;
+                if (a.work) a.work[i] = a.work_rounds ? rounds : nodes;
             }
         }
     }

@@ -4,6 +4,7 @@
 // workspaces, HIP event pairs for kernel timing, options) behind a mutex.  No
 // CPU compute path exists: every board is checked / solved by a HIP kernel.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -58,9 +59,18 @@ struct sdk_ctx {
     uint64_t budget = 0;
     int waves_per_cu = 32;
     int check_blocks_per_cu = 3;
+    int work_rounds = 0;
     // workspaces
     DevBuf stack, counter, in, mask, out, status, work, verdict;
-    DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status;
+    DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask;
+    // the device-resident frontier of the last sdk_frontier_build (in fr_a)
+    uint64_t fr_size = 0;
+    uint64_t fr_leaves = 0;
+    bool fr_valid = false;
+    // RCCL communicator (sdk_comm_init), one rank per context
+    ncclComm_t comm = nullptr;
+    int comm_rank = 0;
+    int comm_world = 1;
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     size_t events_used = 0;
@@ -108,7 +118,8 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
 
 int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
                  uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
-                 unsigned long long* d_counts = nullptr) {
+                 unsigned long long* d_counts = nullptr, uint64_t in_first = 0, uint64_t in_step = 1,
+                 int order = -1) {
     if (n == 0) return SDK_OK;
     if (n > 0x7FFFFFFFull) return fail(SDK_EINVAL, "at most 2^31-1 boards per call");
     const uint64_t slots = (uint64_t)c->cus * c->waves_per_cu;
@@ -132,12 +143,15 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.next = static_cast<uint32_t*>(c->counter.p);
     a.stack = static_cast<uint32_t*>(c->stack.p);
     a.budget = c->budget;
-    a.order = c->order;
+    a.order = order >= 0 ? order : c->order;
     a.limit = limit;
     a.count = d_count;
     a.counts = d_counts;
     a.count_mode = count_mode;
     a.chunk = chunk;
+    a.work_rounds = c->work_rounds;
+    a.in_first = in_first;
+    a.in_step = in_step;
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
     if (rc) return rc;
@@ -147,31 +161,32 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     return SDK_OK;
 }
 
-// Whole-tree solution count with a replicated, deterministic BFS frontier.
-// Every rank expands the same frontier (no exchange), counts the subtrees of its
-// contiguous slice with the batched count kernel; rank 0 also owns the leaves
-// solved during expansion.  The caller sums the per-rank counts.
-int count_frontier(sdk_ctx* c, const uint8_t* h_board, uint64_t limit, int rank, int world, uint64_t* local_count,
-                   uint64_t* frontier_size, int8_t* status) {
-    if (world < 1 || rank < 0 || rank >= world) return fail(SDK_EINVAL, "bad rank %d / world %d", rank, world);
+// Deterministic breadth-first frontier of one board, left in c->fr_a.
+// Every rank that builds it from the same board gets the same boards in the same
+// order, so ranks can split it without exchanging boards.
+//   SDK_FRONTIER_COUNT: MRV branching; solved leaves are counted (fr_leaves) and dropped.
+//   SDK_FRONTIER_FIRST: lex branching, solved leaves kept in place, so the frontier is
+//                       in lex order of completions (see frontier_kernel.h).
+// Expansion stops once the frontier holds >= target boards (or nothing branches).
+int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, int mode, uint64_t target) {
     int rc;
-    // counters: [0] next (u32), [1] leaves (u64), [2] scan total (u64), [3] count total (u64)
-    if ((rc = ensure(c->counter, 256)) || (rc = ensure(c->fr_a, 81))) return rc;
+    c->fr_valid = false;
+    // counters: [0] next (u32), [1] level leaves (u64), [2] scan total, [3] count total, [4] level open
+    if ((rc = ensure(c->counter, 256)) || (rc = ensure(c->fr_a, 81)) || (rc = ensure(c->fr_mask, 16))) return rc;
     unsigned long long* ctr = static_cast<unsigned long long*>(c->counter.p);
-    unsigned long long* d_leaves = ctr + 1;
-    unsigned long long* d_total = ctr + 2;
-    unsigned long long* d_count = ctr + 3;
-    HIPCALL(hipMemsetAsync(c->counter.p, 0, 256, c->stream));
     HIPCALL(hipMemcpyAsync(c->fr_a.p, h_board, 81, hipMemcpyHostToDevice, c->stream));
-    const uint64_t target = (uint64_t)c->cus * (uint64_t)c->waves_per_cu * 8ull * (uint64_t)world;
+    if (h_mask) HIPCALL(hipMemcpyAsync(c->fr_mask.p, h_mask, 2, hipMemcpyHostToDevice, c->stream));
+    if (target == 0) target = (uint64_t)c->cus * (uint64_t)c->waves_per_cu * 8ull;
     const uint64_t cap = 1ull << 25;  // 32M boards (2.6 GB) per frontier buffer
-    uint64_t m = 1;
+    const bool first = mode == SDK_FRONTIER_FIRST;
+    uint64_t m = 1, leaves = 0;
     int level = 0;
-    while (m > 0 && m < target && level < 81) {
+    // a first-cell mask lives only in level 0's expansion: that level always runs
+    while (m > 0 && (m < target || (level == 0 && h_mask)) && level < 81) {
         if ((rc = ensure(c->prop, m * 81)) || (rc = ensure(c->bcell, m)) || (rc = ensure(c->bmask, m * 2)) ||
             (rc = ensure(c->nchild, m * 4)) || (rc = ensure(c->offs, m * 8)))
             return rc;
-        HIPCALL(hipMemsetAsync(c->counter.p, 0, 4, c->stream));
+        HIPCALL(hipMemsetAsync(c->counter.p, 0, 40, c->stream));
         sdk::ExpandArgs ea;
         ea.in = static_cast<const uint8_t*>(c->fr_a.p);
         ea.m = m;
@@ -179,9 +194,12 @@ int count_frontier(sdk_ctx* c, const uint8_t* h_board, uint64_t limit, int rank,
         ea.bcell = static_cast<uint8_t*>(c->bcell.p);
         ea.bmask = static_cast<uint16_t*>(c->bmask.p);
         ea.nchild = static_cast<uint32_t*>(c->nchild.p);
-        ea.leaves = d_leaves;
+        ea.leaves = ctr + 1;
+        ea.open = ctr + 4;
         ea.next = static_cast<uint32_t*>(c->counter.p);
-        ea.order = sdk::ORDER_MRV;
+        ea.order = first ? sdk::ORDER_LEX : sdk::ORDER_MRV;
+        ea.mask = (level == 0 && h_mask) ? static_cast<const uint16_t*>(c->fr_mask.p) : nullptr;
+        ea.keep_leaves = first ? 1 : 0;
         const unsigned eg = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m + sdk::kChunk - 1) / sdk::kChunk,
                                                                                (uint64_t)c->cus * c->waves_per_cu));
         hipEvent_t stop;
@@ -189,14 +207,16 @@ int count_frontier(sdk_ctx* c, const uint8_t* h_board, uint64_t limit, int rank,
         sdk::expand_kernel<<<eg, 64, 0, c->stream>>>(ea);
         HIPCALL(hipGetLastError());
         sdk::scan_kernel<<<1, 1024, 0, c->stream>>>(static_cast<uint32_t*>(c->nchild.p),
-                                                    static_cast<uint64_t*>(c->offs.p), m, d_total);
+                                                    static_cast<uint64_t*>(c->offs.p), m, ctr + 2);
         HIPCALL(hipGetLastError());
-        unsigned long long total = 0;
-        HIPCALL(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, c->stream));
+        unsigned long long h[5] = {0, 0, 0, 0, 0};
+        HIPCALL(hipMemcpyAsync(h, c->counter.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
         HIPCALL(hipStreamSynchronize(c->stream));
+        const uint64_t total = h[2], lvl_leaves = h[1], open = h[4];
+        // level rejected: its children would not fit; fr_a stays as it is
         if (total > cap) {
             HIPCALL(hipEventRecord(stop, c->stream));
-            break;  // keep the current frontier: it is already big enough to split
+            break;
         }
         if (total && (rc = ensure(c->fr_b, total * 81))) return rc;
         if (total) {
@@ -210,37 +230,88 @@ int count_frontier(sdk_ctx* c, const uint8_t* h_board, uint64_t limit, int rank,
         HIPCALL(hipEventRecord(stop, c->stream));
         std::swap(c->fr_a, c->fr_b);
         m = total;
+        leaves += lvl_leaves;
         ++level;
+        if (first && open == 0) break;   // nothing branched: the next level would equal this one
     }
-    // count this rank's slice of the final frontier
-    const uint64_t lo = (rank * m) / world, hi = ((rank + 1) * m) / world;
-    int8_t st = 1;
-    uint64_t cnt = 0;
-    if (hi > lo) {
-        if ((rc = ensure(c->fr_status, hi - lo))) return rc;
-        rc = launch_solve(c, static_cast<uint8_t*>(c->fr_a.p) + lo * 81, nullptr, nullptr,
-                          static_cast<int8_t*>(c->fr_status.p), nullptr, hi - lo, 1, limit, d_count, nullptr);
-        if (rc) return rc;
-        std::vector<int8_t> sts(hi - lo);
-        HIPCALL(hipMemcpyAsync(sts.data(), c->fr_status.p, hi - lo, hipMemcpyDeviceToHost, c->stream));
-        unsigned long long tot = 0;
-        HIPCALL(hipMemcpyAsync(&tot, d_count, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCALL(hipStreamSynchronize(c->stream));
-        cnt = tot;
-        for (int8_t x : sts)
-            if (x == -2) st = -2;
-    }
-    unsigned long long leaves = 0;
-    HIPCALL(hipMemcpyAsync(&leaves, d_leaves, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCALL(hipStreamSynchronize(c->stream));
-    if (rank == 0) cnt += leaves;
-    if (limit && cnt > limit) cnt = limit;
-    if (st != -2) st = cnt > 0 ? 1 : 0;
-    *local_count = cnt;
-    if (frontier_size) *frontier_size = m;
-    *status = st;
+    c->fr_size = m;
+    c->fr_leaves = leaves;
+    c->fr_valid = true;
     return SDK_OK;
 }
+
+// Count the completions below frontier boards first, first+step, ... < end into
+// d_result = {count (u64), boards that hit the node budget (u64)}.
+int frontier_count(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t end, uint64_t limit,
+                   unsigned long long* d_result) {
+    if (!c->fr_valid) return fail(SDK_EINVAL, "no frontier: call sdk_frontier_build first");
+    if (step == 0) return fail(SDK_EINVAL, "step must be >= 1");
+    end = std::min(end, c->fr_size);
+    const uint64_t n = first < end ? (end - first + step - 1) / step : 0;
+    int rc;
+    if ((rc = ensure(c->counter, 256)) || (rc = ensure(c->fr_status, std::max<uint64_t>(n, 1)))) return rc;
+    unsigned long long* d_count = static_cast<unsigned long long*>(c->counter.p) + 3;
+    HIPCALL(hipMemsetAsync(d_count, 0, 8, c->stream));
+    if (n) {
+        rc = launch_solve(c, static_cast<uint8_t*>(c->fr_a.p), nullptr, nullptr, static_cast<int8_t*>(c->fr_status.p),
+                          nullptr, n, 1, limit, d_count, nullptr, first, step);
+        if (rc) return rc;
+    }
+    sdk::count_result_kernel<<<1, 256, 0, c->stream>>>(static_cast<int8_t*>(c->fr_status.p), n, d_count, d_result);
+    HIPCALL(hipGetLastError());
+    return SDK_OK;
+}
+
+// Lex-ordered scan step of a first-solution search: solve frontier boards [lo, hi)
+// and leave the lowest hit in d_found / d_best (first_hit_kernel).
+int frontier_first(sdk_ctx* c, uint64_t lo, uint64_t hi, long long* d_found, uint8_t* d_best) {
+    if (!c->fr_valid) return fail(SDK_EINVAL, "no frontier: call sdk_frontier_build first");
+    hi = std::min(hi, c->fr_size);
+    const uint64_t n = lo < hi ? hi - lo : 0;
+    int rc;
+    if ((rc = ensure(c->out, std::max<uint64_t>(n, 1) * 81)) || (rc = ensure(c->status, std::max<uint64_t>(n, 1))))
+        return rc;
+    if (n) {
+        rc = launch_solve(c, static_cast<uint8_t*>(c->fr_a.p), nullptr, static_cast<uint8_t*>(c->out.p),
+                          static_cast<int8_t*>(c->status.p), nullptr, n, 0, 0, nullptr, nullptr, lo, 1);
+        if (rc) return rc;
+    }
+    sdk::first_hit_kernel<<<1, 256, 0, c->stream>>>(static_cast<int8_t*>(c->status.p),
+                                                    static_cast<uint8_t*>(c->out.p), n, lo, d_found, d_best);
+    HIPCALL(hipGetLastError());
+    return SDK_OK;
+}
+
+// Single-process form of the frontier count (sdk_count_solutions[_slice]): this
+// rank's contiguous slice; rank 0 adds the leaves met during expansion.
+int count_slice(sdk_ctx* c, const uint8_t* h_board, uint64_t limit, int rank, int world, uint64_t* local_count,
+                uint64_t* frontier_size, int8_t* status) {
+    if (world < 1 || rank < 0 || rank >= world) return fail(SDK_EINVAL, "bad rank %d / world %d", rank, world);
+    int rc = build_frontier(c, h_board, nullptr, SDK_FRONTIER_COUNT,
+                            (uint64_t)c->cus * (uint64_t)c->waves_per_cu * 8ull * (uint64_t)world);
+    if (rc) return rc;
+    const uint64_t m = c->fr_size;
+    const uint64_t lo = (rank * m) / world, hi = ((rank + 1) * m) / world;
+    unsigned long long* d_res = static_cast<unsigned long long*>(c->counter.p) + 6;
+    if ((rc = frontier_count(c, lo, 1, hi, limit, d_res))) return rc;
+    unsigned long long res[2] = {0, 0};
+    HIPCALL(hipMemcpyAsync(res, d_res, sizeof res, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    uint64_t cnt = res[0] + (rank == 0 ? c->fr_leaves : 0);
+    if (limit && cnt > limit) cnt = limit;
+    *local_count = cnt;
+    if (frontier_size) *frontier_size = m;
+    *status = res[1] ? (int8_t)-2 : (cnt > 0 ? (int8_t)1 : (int8_t)0);
+    return SDK_OK;
+}
+
+#define NCCLCALL(expr)                                                                        \
+    do {                                                                                      \
+        ncclResult_t r_ = (expr);                                                             \
+        if (r_ != ncclSuccess)                                                                \
+            return fail(SDK_ECOMM, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, __LINE__); \
+    } while (0)
 
 }  // namespace
 
@@ -287,8 +358,10 @@ int sdk_destroy(sdk_ctx* c) {
     if (!c) return SDK_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
     for (DevBuf* b : {&c->stack, &c->counter, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
-                      &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status})
+                      &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status,
+                      &c->fr_mask})
         if (b->p) (void)hipFree(b->p);
     for (auto& pr : c->events) {
         (void)hipEventDestroy(pr.first);
@@ -319,6 +392,12 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 1 || value > 16) return fail(SDK_EINVAL, "check blocks per CU must be 1..16");
             c->check_blocks_per_cu = (int)value;
             return SDK_OK;
+        case SDK_OPT_WORK_COUNTER:
+            if (value != SDK_WORK_NODES && value != SDK_WORK_ROUNDS) return fail(SDK_EINVAL, "bad work counter %lld", (long long)value);
+            c->work_rounds = (int)value;
+            return SDK_OK;
+        case SDK_OPT_DEVICE_CUS:
+            return fail(SDK_EINVAL, "SDK_OPT_DEVICE_CUS is read-only");
         default:
             return fail(SDK_EINVAL, "unknown option %d", key);
     }
@@ -332,6 +411,8 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_NODE_BUDGET: *value = (int64_t)c->budget; return SDK_OK;
         case SDK_OPT_WAVES_PER_CU: *value = c->waves_per_cu; return SDK_OK;
         case SDK_OPT_CHECK_BLOCKS_PER_CU: *value = c->check_blocks_per_cu; return SDK_OK;
+        case SDK_OPT_WORK_COUNTER: *value = c->work_rounds; return SDK_OK;
+        case SDK_OPT_DEVICE_CUS: *value = c->cus; return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }
 }
@@ -461,7 +542,7 @@ int sdk_count_solutions(sdk_ctx* c, const uint8_t* board, uint64_t limit, uint64
     if (!c || !board || !count || !status) return fail(SDK_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
-    return count_frontier(c, board, limit, 0, 1, count, nullptr, status);
+    return count_slice(c, board, limit, 0, 1, count, nullptr, status);
 }
 
 int sdk_count_solutions_slice(sdk_ctx* c, const uint8_t* board, uint64_t limit, int rank, int world,
@@ -469,7 +550,103 @@ int sdk_count_solutions_slice(sdk_ctx* c, const uint8_t* board, uint64_t limit, 
     if (!c || !board || !count || !status) return fail(SDK_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
-    return count_frontier(c, board, limit, rank, world, count, frontier_size, status);
+    return count_slice(c, board, limit, rank, world, count, frontier_size, status);
+}
+
+int sdk_frontier_build(sdk_ctx* c, const uint8_t* board, const uint16_t* first_cell_mask, int mode, uint64_t target,
+                       uint64_t* size, uint64_t* leaves) {
+    if (!c || !board) return fail(SDK_EINVAL, "NULL argument");
+    if (mode != SDK_FRONTIER_COUNT && mode != SDK_FRONTIER_FIRST) return fail(SDK_EINVAL, "bad frontier mode %d", mode);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    int rc = build_frontier(c, board, first_cell_mask, mode, target);
+    if (rc) return rc;
+    if (size) *size = c->fr_size;
+    if (leaves) *leaves = c->fr_leaves;
+    return SDK_OK;
+}
+
+int sdk_frontier_count_dev(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t end, uint64_t limit, void* d_result) {
+    if (!c || !d_result) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    return frontier_count(c, first, step, end, limit, static_cast<unsigned long long*>(d_result));
+}
+
+int sdk_frontier_first_dev(sdk_ctx* c, uint64_t lo, uint64_t hi, void* d_found, void* d_best) {
+    if (!c || !d_found || !d_best) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    return frontier_first(c, lo, hi, static_cast<long long*>(d_found), static_cast<uint8_t*>(d_best));
+}
+
+int sdk_comm_unique_id(uint8_t* id) {
+    if (!id) return fail(SDK_EINVAL, "NULL argument");
+    ncclUniqueId u;
+    NCCLCALL(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, SDK_COMM_ID_BYTES);
+    return SDK_OK;
+}
+
+int sdk_comm_init(sdk_ctx* c, const uint8_t* id, int rank, int world) {
+    if (!c || !id) return fail(SDK_EINVAL, "NULL argument");
+    if (world < 1 || rank < 0 || rank >= world) return fail(SDK_EINVAL, "bad rank %d / world %d", rank, world);
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->comm) return fail(SDK_EINVAL, "context already has a communicator");
+    HIPCALL(hipSetDevice(c->device));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, SDK_COMM_ID_BYTES);
+    NCCLCALL(ncclCommInitRank(&c->comm, world, u, rank));
+    c->comm_rank = rank;
+    c->comm_world = world;
+    return SDK_OK;
+}
+
+int sdk_comm_destroy(sdk_ctx* c) {
+    if (!c) return fail(SDK_EINVAL, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->comm) return SDK_OK;
+    HIPCALL(hipSetDevice(c->device));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    ncclComm_t comm = c->comm;
+    c->comm = nullptr;
+    c->comm_rank = 0;
+    c->comm_world = 1;
+    NCCLCALL(ncclCommDestroy(comm));
+    return SDK_OK;
+}
+
+int sdk_comm_allreduce_dev(sdk_ctx* c, void* d_buf, size_t count, int dtype, int op) {
+    if (!c || (count && !d_buf)) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->comm) return fail(SDK_EINVAL, "no communicator: call sdk_comm_init first");
+    ncclDataType_t t;
+    switch (dtype) {
+        case SDK_COMM_U64: t = ncclUint64; break;
+        case SDK_COMM_I64: t = ncclInt64; break;
+        case SDK_COMM_U8: t = ncclUint8; break;
+        default: return fail(SDK_EINVAL, "bad dtype %d", dtype);
+    }
+    ncclRedOp_t o;
+    switch (op) {
+        case SDK_COMM_SUM: o = ncclSum; break;
+        case SDK_COMM_MIN: o = ncclMin; break;
+        case SDK_COMM_MAX: o = ncclMax; break;
+        default: return fail(SDK_EINVAL, "bad op %d", op);
+    }
+    HIPCALL(hipSetDevice(c->device));
+    NCCLCALL(ncclAllReduce(d_buf, d_buf, count, t, o, c->comm, c->stream));
+    return SDK_OK;
+}
+
+int sdk_comm_broadcast_dev(sdk_ctx* c, void* d_buf, size_t bytes, int root) {
+    if (!c || (bytes && !d_buf)) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->comm) return fail(SDK_EINVAL, "no communicator: call sdk_comm_init first");
+    if (root < 0 || root >= c->comm_world) return fail(SDK_EINVAL, "bad root %d", root);
+    HIPCALL(hipSetDevice(c->device));
+    NCCLCALL(ncclBroadcast(d_buf, d_buf, bytes, ncclUint8, root, c->comm, c->stream));
+    return SDK_OK;
 }
 
 }  // extern "C"

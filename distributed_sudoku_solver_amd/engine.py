@@ -208,6 +208,59 @@ class SudokuEngine:
                 "sdk_count_solutions_slice")
         return cnt.value, fr.value, st.value
 
+    # ------------------------------------------- one-board multi-GPU searches
+    def frontier_build(self, board, mask=None, mode=L.SDK_FRONTIER_COUNT, target=0):
+        """Build the deterministic frontier of `board` on this GPU: (size, leaves)."""
+        board = np.ascontiguousarray(board, dtype=np.uint8).reshape(81)
+        m = None if mask is None else np.array([int(mask)], dtype=np.uint16)
+        size = ctypes.c_uint64()
+        leaves = ctypes.c_uint64()
+        L.check(self.lib.sdk_frontier_build(self.ctx, _ptr(board), _ptr(m), int(mode), int(target),
+                                            ctypes.byref(size), ctypes.byref(leaves)), "sdk_frontier_build")
+        return size.value, leaves.value
+
+    def frontier_count(self, first, step, end, limit, d_result):
+        """Completions below frontier boards first, first+step, ... < end -> d_result {count, budget hits}."""
+        L.check(self.lib.sdk_frontier_count_dev(self.ctx, int(first), int(step), int(end), int(limit), d_result.ptr),
+                "sdk_frontier_count_dev")
+
+    def frontier_first(self, lo, hi, d_found, d_best):
+        """Lex-ordered scan step: lowest hit index in [lo, hi) -> d_found, its board + status -> d_best."""
+        L.check(self.lib.sdk_frontier_first_dev(self.ctx, int(lo), int(hi), d_found.ptr, d_best.ptr),
+                "sdk_frontier_first_dev")
+
+    def result_buffer(self, count, dtype):
+        """A small device buffer for per-rank results (a handle for the comm layer)."""
+        buf = self.alloc(count * np.dtype(dtype).itemsize)
+        buf.upload(np.zeros(count, dtype=dtype))
+        return buf
+
+    def read(self, buf, count, dtype):
+        out = np.empty(count, dtype=dtype)
+        return buf.download(out)
+
+    # ----------------------------------------------------------------- RCCL
+    @staticmethod
+    def comm_unique_id():
+        lib = L.load()
+        buf = (ctypes.c_uint8 * L.SDK_COMM_ID_BYTES)()
+        L.check(lib.sdk_comm_unique_id(buf), "sdk_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, uid, rank, world):
+        buf = (ctypes.c_uint8 * L.SDK_COMM_ID_BYTES).from_buffer_copy(uid)
+        L.check(self.lib.sdk_comm_init(self.ctx, buf, int(rank), int(world)), "sdk_comm_init")
+
+    def comm_destroy(self):
+        L.check(self.lib.sdk_comm_destroy(self.ctx), "sdk_comm_destroy")
+
+    def comm_allreduce(self, d_buf, count, dtype, op):
+        L.check(self.lib.sdk_comm_allreduce_dev(self.ctx, d_buf.ptr, int(count), int(dtype), int(op)),
+                "sdk_comm_allreduce_dev")
+
+    def comm_broadcast(self, d_buf, nbytes, root):
+        L.check(self.lib.sdk_comm_broadcast_dev(self.ctx, d_buf.ptr, int(nbytes), int(root)), "sdk_comm_broadcast_dev")
+
     # --------------------------------------------------------- device batch
     def check_batch_dev(self, d_boards, d_verdict, n):
         L.check(self.lib.sdk_check_batch_dev(self.ctx, d_boards.ptr, d_verdict.ptr, int(n)), "sdk_check_batch_dev")

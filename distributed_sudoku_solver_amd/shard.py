@@ -12,14 +12,30 @@ Two front ends:
   * MultiDeviceEngine: one process driving several GPUs from threads (ctypes
     releases the GIL for the duration of each library call).
 
-Whole-tree counts of ONE board split a replicated,
-deterministic BFS frontier instead (sharded_count): every rank expands the same
-frontier on its GPU, counts its slice, and the only exchange is one all-reduce
-of a 64-bit count (plus a min of the status) across ranks.
+Searches of ONE board split a replicated,
+deterministic breadth-first frontier instead -- the in-node form of the
+reference's DFS subtree hand-off (NEEDWORK -> TASK with half of the digit range
+and a partial board, DHT_Node.py:491-510, 225-250; utils.py:1-9):
+  * sharded_count: every rank expands the same frontier on its GPU, counts the
+    boards i = rank, rank+world, ... (interleaved for load balance), and the only
+    exchange is one RCCL all-reduce of {count, budget hits} in device memory.
+  * sharded_solve: first solution in the reference's DFS order.  The frontier is
+    built in lex order; ranks scan it in interleaved chunks, wave by wave, and
+    after each wave an RCCL all-reduce(min) of the lowest hit index is the
+    found/termination flag; the owner of that index broadcasts the board.  Lower
+    chunks always finish before a higher hit is accepted, so the answer is
+    identical for every world size.
+The collectives go through a `comm` object: RcclComm (device memory, RCCL over
+xGMI, the product path) or HostComm (host arrays over any torch.distributed
+group, used by the CPU tests with a stand-in engine).
 """
 import threading
 
 import numpy as np
+
+from . import _lib as L
+
+INT64_MAX = (1 << 63) - 1
 
 
 def shard_bounds(n, rank, world):
@@ -139,30 +155,131 @@ class MultiDeviceEngine:
         return v
 
 
-def allreduce_gloo(values, op="sum", group=None):
-    """Host all-reduce of a few int64 scalars over torch.distributed (any backend
-    that takes CPU tensors, e.g. gloo).  Returns a list of ints."""
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([int(v) for v in values], dtype=torch.int64)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MIN, group=group)
-    return [int(x) for x in t.tolist()]
+class RcclComm:
+    """RCCL communicator of one engine (one rank per GPU).  The 128-byte id is made
+    by rank 0 and handed to the other ranks over an existing torch.distributed
+    group (gloo is enough: it is 128 bytes once)."""
+
+    _DT = {np.dtype(np.uint64): L.SDK_COMM_U64, np.dtype(np.int64): L.SDK_COMM_I64,
+           np.dtype(np.uint8): L.SDK_COMM_U8}
+    _OP = {"sum": L.SDK_COMM_SUM, "min": L.SDK_COMM_MIN, "max": L.SDK_COMM_MAX}
+
+    def __init__(self, engine, rank, world, group=None, uid=None):
+        self.engine, self.rank, self.world = engine, rank, world
+        if uid is None:
+            uid = self.exchange_id(rank, group)
+        engine.comm_init(uid, rank, world)
+
+    @staticmethod
+    def exchange_id(rank, group=None):
+        import torch
+        import torch.distributed as dist
+        from .engine import SudokuEngine
+        t = torch.zeros(L.SDK_COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            t[:] = torch.frombuffer(bytearray(SudokuEngine.comm_unique_id()), dtype=torch.uint8)
+        dist.broadcast(t, src=0, group=group)
+        return bytes(t.numpy().tobytes())
+
+    def allreduce(self, buf, count, dtype, op):
+        self.engine.comm_allreduce(buf, count, self._DT[np.dtype(dtype)], self._OP[op])
+
+    def broadcast(self, buf, nbytes, root):
+        self.engine.comm_broadcast(buf, nbytes, root)
+
+    def close(self):
+        self.engine.comm_destroy()
 
 
-def sharded_count(engine, board, rank, world, limit=0, allreduce=None):
+class HostComm:
+    """Same interface over host numpy arrays and a torch.distributed group (gloo):
+    the CPU stand-in for RcclComm in multi-process tests."""
+
+    _OPS = {"sum": "SUM", "min": "MIN", "max": "MAX"}
+
+    def __init__(self, rank, world, group=None):
+        self.rank, self.world, self.group = rank, world, group
+
+    def allreduce(self, buf, count, dtype, op):
+        import torch
+        import torch.distributed as dist
+        t = torch.from_numpy(buf[:count].astype(np.int64))
+        dist.all_reduce(t, op=getattr(dist.ReduceOp, self._OPS[op]), group=self.group)
+        buf[:count] = t.numpy().astype(buf.dtype)
+
+    def broadcast(self, buf, nbytes, root):
+        import torch
+        import torch.distributed as dist
+        t = torch.from_numpy(buf.view(np.uint8)[:nbytes].copy())
+        dist.broadcast(t, src=root, group=self.group)
+        buf.view(np.uint8)[:nbytes] = t.numpy()
+
+    def close(self):
+        pass
+
+
+def default_target(engine, world):
+    """Frontier size: 8 boards per resident solver wave per GPU."""
+    return engine.get_option(L.SDK_OPT_DEVICE_CUS) * engine.get_option(L.SDK_OPT_WAVES_PER_CU) * 8 * world
+
+
+def sharded_count(engine, board, rank, world, limit=0, comm=None, target=None):
     """Count the completions of `board` with `world` ranks (one GPU each).
 
-    Returns (total, status, frontier_size).  `allreduce(values, op)` combines
-    scalars across ranks (default: allreduce_gloo when world > 1)."""
-    local, frontier, st = engine.count_solutions_slice(board, rank, world, limit)
-    if world > 1:
-        red = allreduce or allreduce_gloo
-        total = red([local], "sum")[0]
-        st = red([st], "min")[0]
-    else:
-        total = local
+    Returns (total, status, frontier_size); status 1 = >= 1 completion, 0 = none,
+    -2 = some subtree hit the node budget (total is then a lower bound)."""
+    if world > 1 and comm is None:
+        raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
+    size, leaves = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT,
+                                         target=default_target(engine, world) if target is None else target)
+    res = engine.result_buffer(2, np.uint64)
+    try:
+        engine.frontier_count(rank, world, size, limit, res)       # boards rank, rank+world, ...
+        if comm is not None:
+            comm.allreduce(res, 2, np.uint64, "sum")
+        count, hits = (int(x) for x in engine.read(res, 2, np.uint64))
+    finally:
+        if hasattr(res, "free"):
+            res.free()
+    total = count + leaves                                         # leaves: same on every rank
     if limit and total > limit:
         total = limit
-    if st != -2:
-        st = 1 if total > 0 else 0
-    return total, st, frontier
+    st = -2 if hits else (1 if total > 0 else 0)
+    return total, st, size
+
+
+def sharded_solve(engine, board, rank, world, comm=None, mask=None, waves=8, target=None):
+    """First completion of `board` in the reference's DFS order, split over `world` ranks.
+
+    Returns (out uint8[81], status) with solve_sudoku's contract: the lex-first
+    completion and 1, or the input and 0 (no completion) / -2 (node budget hit in
+    a subtree that precedes every completion found)."""
+    if world > 1 and comm is None:
+        raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
+    board = np.ascontiguousarray(board, dtype=np.uint8).reshape(81)
+    size, _ = engine.frontier_build(board, mask=mask, mode=L.SDK_FRONTIER_FIRST,
+                                    target=default_target(engine, world) if target is None else target)
+    if size == 0:
+        return board.copy(), 0
+    chunk = max(1, -(-size // (world * waves)))
+    nchunks = -(-size // chunk)
+    found = engine.result_buffer(1, np.int64)
+    best = engine.result_buffer(82, np.uint8)
+    try:
+        for wave in range(-(-nchunks // world)):
+            k = wave * world + rank
+            engine.frontier_first(k * chunk, min((k + 1) * chunk, size), found, best)
+            if comm is not None:
+                comm.allreduce(found, 1, np.int64, "min")         # found / termination flag
+            g = int(engine.read(found, 1, np.int64)[0])
+            if g != INT64_MAX:
+                if comm is not None:
+                    comm.broadcast(best, 82, (g // chunk) % world)
+                b = engine.read(best, 82, np.uint8)
+                st = int(b[81].view(np.int8))
+                return (b[:81].copy() if st == 1 else board.copy()), st
+    finally:
+        for h in (found, best):
+            if hasattr(h, "free"):
+                h.free()
+    return board.copy(), 0

@@ -14,6 +14,9 @@
  *       -> sdk_check_batch / sdk_check_batch_dev
  *   (no reference counterpart)
  *       -> sdk_count_solutions
+ *   DFS subtree split across ring nodes (NEEDWORK/TASK, DHT_Node.py:491-510,
+ *   225-250; utils.py:1-9) -- within one node of GPUs:
+ *       -> sdk_frontier_* + sdk_comm_* (RCCL over xGMI)
  *
  * Conventions
  *   - Boards are uint8_t[81], row-major, 0 = empty, 1..9 = given digit,
@@ -46,6 +49,7 @@ extern "C" {
 #define SDK_EINVAL   -1   /* bad argument */
 #define SDK_EHIP     -2   /* HIP runtime failure (message in sdk_last_error) */
 #define SDK_ENOMEM   -3   /* device or host allocation failed */
+#define SDK_ECOMM    -4   /* RCCL failure (message in sdk_last_error) */
 
 /* per-board solve status (int8_t) */
 #define SDK_SOLVED        1   /* out = lexicographically first completion          */
@@ -62,6 +66,11 @@ extern "C" {
 #define SDK_OPT_NODE_BUDGET  2  /* max search nodes per board, 0 = unlimited          */
 #define SDK_OPT_WAVES_PER_CU 3  /* solver residency, 1..32 (default 32)               */
 #define SDK_OPT_CHECK_BLOCKS_PER_CU 4 /* checker grid = CUs x this, 1..16 (default 3)  */
+#define SDK_OPT_WORK_COUNTER 5  /* what solve `work` counts: SDK_WORK_* (default nodes) */
+#define SDK_OPT_DEVICE_CUS   6  /* read-only: compute units of the context's GPU        */
+
+#define SDK_WORK_NODES       0  /* search nodes (propagation fixpoints)                */
+#define SDK_WORK_ROUNDS      1  /* propagation rounds (profiling)                      */
 
 #define SDK_ORDER_MRV_UNIQUE 0  /* MRV search for <=2 solutions; lex re-search if >=2 */
 #define SDK_ORDER_LEX        1  /* lowest-index branching after propagation            */
@@ -109,6 +118,55 @@ int sdk_count_solutions(sdk_ctx *ctx, const uint8_t *board, uint64_t limit,
  * all-reduce it).  frontier_size (nullable) = boards in the split frontier. */
 int sdk_count_solutions_slice(sdk_ctx *ctx, const uint8_t *board, uint64_t limit, int rank, int world,
                               uint64_t *count, uint64_t *frontier_size, int8_t *status);
+
+/* ---- multi-GPU searches of ONE board ---------------------
+ *
+ * Every rank builds the same deterministic breadth-first frontier of the board
+ * on its own GPU (no exchange), works on its share of it, and combines results
+ * with RCCL collectives on device memory, enqueued on the context stream.
+ *
+ *   SDK_FRONTIER_COUNT  MRV branching; completions met while expanding are
+ *                       counted in *leaves (identical on every rank) and dropped.
+ *   SDK_FRONTIER_FIRST  lowest-open-cell branching, digits ascending, solved
+ *                       boards kept: frontier index order = the reference's DFS
+ *                       order (DHT_Node.py:522), so the first frontier board with
+ *                       a completion holds the reference's answer.  The digit
+ *                       mask (nullable) restricts the lowest empty cell of
+ *                       `board`, like a TASK `range`.
+ * target = frontier size to reach (0 = 8 boards per resident solver wave). */
+#define SDK_FRONTIER_COUNT 0
+#define SDK_FRONTIER_FIRST 1
+int sdk_frontier_build(sdk_ctx *ctx, const uint8_t *board, const uint16_t *first_cell_mask, int mode,
+                       uint64_t target, uint64_t *size, uint64_t *leaves);
+
+/* Count mode: completions below frontier boards first, first+step, ... < end,
+ * written to d_result (device, 2 x uint64): {count, boards that hit the node
+ * budget}.  The per-board search stops the batch once count >= limit (0 = none). */
+int sdk_frontier_count_dev(sdk_ctx *ctx, uint64_t first, uint64_t step, uint64_t end, uint64_t limit,
+                           void *d_result);
+
+/* First mode: solve frontier boards [lo, hi) (each to its lex-first completion)
+ * and write the lowest index whose status is not SDK_UNSOLVABLE to d_found
+ * (device int64; INT64_MAX if none) and that board's output + status to d_best
+ * (device, 82 bytes: board[81], int8 status). */
+int sdk_frontier_first_dev(sdk_ctx *ctx, uint64_t lo, uint64_t hi, void *d_found, void *d_best);
+
+/* RCCL communicator bound to a context (one rank per GPU).  Rank 0 makes the
+ * id, the caller distributes it (e.g. over torch.distributed/gloo), every rank
+ * calls sdk_comm_init (collective, blocks until all ranks joined). */
+#define SDK_COMM_ID_BYTES 128
+#define SDK_COMM_U64 0
+#define SDK_COMM_I64 1
+#define SDK_COMM_U8  2
+#define SDK_COMM_SUM 0
+#define SDK_COMM_MIN 1
+#define SDK_COMM_MAX 2
+int sdk_comm_unique_id(uint8_t *id /* SDK_COMM_ID_BYTES */);
+int sdk_comm_init(sdk_ctx *ctx, const uint8_t *id, int rank, int world);
+int sdk_comm_destroy(sdk_ctx *ctx);
+/* In place, on device memory, enqueued on the context stream. */
+int sdk_comm_allreduce_dev(sdk_ctx *ctx, void *d_buf, size_t count, int dtype, int op);
+int sdk_comm_broadcast_dev(sdk_ctx *ctx, void *d_buf, size_t bytes, int root);
 
 /* ---- device-pointer API (asynchronous on the context stream) ------------ */
 int sdk_dev_alloc(sdk_ctx *ctx, size_t bytes, void **dptr);

@@ -200,3 +200,70 @@ def test_frontier_count_matches_oracle_and_slices_partition(engine):
     dead = synth.parse(synth.WIKI).copy(); dead[2] = 5
     assert engine.count_solutions(dead) == (0, 0)
     assert engine.count_solutions(b15, limit=1000)[0] == 1000
+
+
+# ------------------------------------------------ one-board multi-GPU searches
+DEMO = "000100000000320000000009000000000070000000000000900000000000900000000003000000000"
+
+
+def test_frontier_first_solution_matches_reference(engine, solve_cases):
+    """sharded_solve (lex-ordered frontier scan) reproduces every golden solve case,
+    including TASK ranges and unsolvable boards, at several frontier sizes."""
+    from distributed_sudoku_solver_amd.shard import sharded_solve
+    for target in (1, 50, 0):
+        for c in solve_cases[:40]:
+            board = np.array(c["puzzle"], np.uint8)
+            out, st = sharded_solve(engine, board, 0, 1, mask=O.range_mask(*c["range"]), target=target)
+            assert (st == 1) == c["ok"], (c["name"], target)
+            assert out.tolist() == (c["board"] if c["ok"] else c["puzzle"]), (c["name"], target)
+
+
+def test_frontier_first_solution_random_vs_oracle(engine):
+    from distributed_sudoku_solver_amd.shard import sharded_solve
+    puz = _random_puzzles(60, 55, 8, 26)
+    ref_out, ref_st, _ = O.naive_solve_batch(puz, budget=50_000_000, threads=8)
+    for i, b in enumerate(puz):
+        if ref_st[i] == -2:
+            continue
+        out, st = sharded_solve(engine, b, 0, 1, waves=3)
+        assert st == ref_st[i] and (out == ref_out[i]).all(), i
+
+
+def test_frontier_count_interleaved_ranks_partition(engine):
+    """Every world size's interleaved shares sum to the total (the RCCL sum's inputs)."""
+    s1 = synth.SEEDS17["S1"]
+    b16 = synth.parse(s1[:-9] + "000800000")
+    for world in (1, 2, 3, 8):
+        size, leaves = engine.frontier_build(b16, mode=L.SDK_FRONTIER_COUNT, target=1000 * world)
+        total = leaves
+        res = engine.result_buffer(2, np.uint64)
+        for r in range(world):
+            engine.frontier_count(r, world, size, 0, res)
+            cnt, hits = engine.read(res, 2, np.uint64)
+            assert hits == 0
+            total += int(cnt)
+        res.free()
+        assert total == 7309, world
+
+
+def test_rccl_communicator_world1(engine):
+    """RCCL path end to end on one GPU: communicator of size 1, device all-reduce /
+    broadcast inside sharded_count and sharded_solve."""
+    from distributed_sudoku_solver_amd.engine import SudokuEngine
+    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count, sharded_solve
+    eng = SudokuEngine(0)
+    try:
+        comm = RcclComm(eng, 0, 1, uid=SudokuEngine.comm_unique_id())
+        buf = eng.result_buffer(3, np.int64)
+        buf.upload(np.array([5, -7, 9], np.int64))
+        comm.allreduce(buf, 3, np.int64, "min")
+        assert eng.read(buf, 3, np.int64).tolist() == [5, -7, 9]
+        buf.free()
+        s1 = synth.SEEDS17["S1"]
+        assert sharded_count(eng, synth.parse(s1[:-9] + "000800000"), 0, 1, comm=comm)[:2] == (7309, 1)
+        out, st = sharded_solve(eng, synth.parse(DEMO), 0, 1, comm=comm)
+        assert st == 1 and "".join(map(str, out)) == \
+            "234156789179328456568479132391245678425687391687913245752831964816794523943562817"
+        comm.close()
+    finally:
+        eng.close()

@@ -8,8 +8,9 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from distributed_sudoku_solver_amd.shard import MultiDeviceEngine, ShardedBatch, shard_bounds, sharded_count
-from distributed_sudoku_solver_amd import synth
+from distributed_sudoku_solver_amd.shard import (HostComm, MultiDeviceEngine, ShardedBatch, shard_bounds,
+                                                 sharded_count, sharded_solve)
+from distributed_sudoku_solver_amd import synth, _lib as L
 
 
 class OracleEngine:
@@ -29,16 +30,71 @@ class OracleEngine:
         self.calls.append(len(boards))
         return self.O.check_batch(boards, threads=2)
 
-    def count_solutions_slice(self, board, rank, world, limit=0):
-        """Stand-in frontier: the candidates of the first empty cell, split by rank."""
-        b = np.asarray(board, dtype=np.uint8).copy()
-        cell = int(np.flatnonzero(b == 0)[0])
-        cnt = 0
-        for k, d in enumerate(range(1, 10)):
-            if k % world == rank:
-                b[cell] = d
-                cnt += self.O.count(b, limit, 1)
-        return cnt, 9, 1 if cnt else 0
+    # ---- frontier primitives, restated on the CPU (test double of libsudoku_hip's) ----
+    def get_option(self, key):
+        return {L.SDK_OPT_DEVICE_CUS: 1, L.SDK_OPT_WAVES_PER_CU: 2}[key]
+
+    def frontier_build(self, board, mask=None, mode=L.SDK_FRONTIER_COUNT, target=0):
+        """Naive-DFS order expansion (lowest empty cell, digits ascending, utils.py:14-56)
+        without propagation, level by level until >= target boards."""
+        fr = [np.asarray(board, dtype=np.uint8).copy()]
+        allowed0 = mask
+        while fr and len(fr) < max(target, 1):
+            nxt, grew = [], False
+            for b in fr:
+                z = np.flatnonzero(b == 0)
+                if len(z) == 0:
+                    nxt.append(b)
+                    continue
+                grew = True
+                c = int(z[0])
+                r, col = divmod(c, 9)
+                br, bc = 3 * (r // 3), 3 * (col // 3)
+                used = set(b[9 * r: 9 * r + 9]) | set(b[col::9]) | {b[9 * (br + i) + bc + j] for i in range(3)
+                                                                    for j in range(3)}
+                for d in range(1, 10):
+                    if allowed0 is not None and not (allowed0 >> d) & 1:
+                        continue
+                    if d not in used:
+                        ch = b.copy()
+                        ch[c] = d
+                        nxt.append(ch)
+            allowed0 = None
+            fr = nxt
+            if not grew:
+                break
+        self.frontier = fr
+        return len(fr), 0
+
+    def result_buffer(self, count, dtype):
+        return np.zeros(count, dtype=dtype)
+
+    def read(self, buf, count, dtype):
+        return buf[:count].astype(dtype)
+
+    def frontier_count(self, first, step, end, limit, res):
+        idx = list(range(first, min(end, len(self.frontier)), step))
+        self.calls.append(("count", idx))
+        res[0] = sum(self.O.count(self.frontier[i], limit, 1) for i in idx)
+        res[1] = 0
+
+    def frontier_first(self, lo, hi, found, best):
+        hi = min(hi, len(self.frontier))
+        self.calls.append(("first", lo, hi))
+        found[0] = (1 << 63) - 1
+        if hi > lo:
+            out, st, _ = self.O.naive_solve_batch(np.stack(self.frontier[lo:hi]), budget=50_000_000, threads=2)
+            hits = np.flatnonzero(st != 0)
+            if len(hits):
+                i = int(hits[0])
+                found[0] = lo + i
+                best[:81] = out[i]
+                best[81] = np.int8(st[i]).view(np.uint8)
+
+
+def O_range_mask(lo, hi):
+    from oracle import oracle as O
+    return O.range_mask(lo, hi)
 
 
 def _free_port():
@@ -63,11 +119,29 @@ def _worker(rank, world, port, q):
         if rank == 0:
             q.put(("solve", bool((out == s).all() and (st == 1).all())))
             q.put(("check", bool((v == exp).all())))
+        comm = HostComm(rank, world)
         s1 = synth.SEEDS17["S1"]
-        total, st, _ = sharded_count(eng, synth.parse(s1[:-9] + "000800000"), rank, world)
+        q.put(("calls", rank, list(eng.calls)))
+        eng.calls = []
+        total, st, size = sharded_count(eng, synth.parse(s1[:-9] + "000800000"), rank, world, comm=comm)
+        counted = [c[1] for c in eng.calls if c[0] == "count"][0]
         if rank == 0:
-            q.put(("count", total == 7309 and st == 1))
-        q.put(("calls", rank, eng.calls))
+            q.put(("count", total == 7309 and st == 1 and size >= 32))
+        q.put(("count_split", rank, counted, size))
+        # first solution of the multi-solution demo board (sudoku.py:99-109) = reference golden
+        demo = synth.parse("000100000000320000000009000000000070000000000000900000000000900000000003000000000")
+        golden = "234156789179328456568479132391245678425687391687913245752831964816794523943562817"
+        out, st = sharded_solve(eng, demo, rank, world, comm=comm)
+        q.put(("first", rank, "".join(map(str, out)) == golden and st == 1))
+        # TASK range(5, 10) on the same board (golden: reference solve_sudoku with arr=range(5,10))
+        out, st = sharded_solve(eng, demo, rank, world, comm=comm, mask=O_range_mask(5, 10))
+        q.put(("first_range", rank, "".join(map(str, out)) ==
+               "523146789179328456468579132291435678345687291687912345712853964954761823836294517" and st == 1))
+        # unsolvable (clue conflict), the wiki board with (0,1) = 5: input comes back, status 0
+        bad = synth.parse("55" + synth.WIKI[2:])
+        out, st = sharded_solve(eng, bad, rank, world, comm=comm, target=4)
+        q.put(("unsolvable", rank, st == 0 and (out == bad).all()))
+
     finally:
         dist.destroy_process_group()
 
@@ -93,9 +167,14 @@ def test_world2_gloo_gather():
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    got = [q.get(timeout=5) for _ in range(5)]
-    res = {g[0]: g[1:] for g in got if g[0] != "calls"}
+    got = [q.get(timeout=5) for _ in range(3 + 5 * world)]
+    res = {g[0]: g[1:] for g in got if g[0] not in ("calls", "count_split", "first", "first_range", "unsolvable")}
     assert res["solve"] == (True,) and res["check"] == (True,) and res["count"] == (True,)
+    for key in ("first", "first_range", "unsolvable"):
+        assert sorted(g[1:] for g in got if g[0] == key) == [(r, True) for r in range(world)], key
+    split = {g[1]: g[2:] for g in got if g[0] == "count_split"}
+    size = split[0][1]
+    assert sorted(split[0][0] + split[1][0]) == list(range(size))     # interleaved, disjoint, complete
     calls = {g[1]: g[2] for g in got if g[0] == "calls"}
     assert calls[0] == [150, 500] and calls[1] == [151, 501]     # each rank ran only its slice
 

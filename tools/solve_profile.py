@@ -1,0 +1,50 @@
+"""Solve-kernel profiling driver (dev tool, not a test): timing, search nodes and propagation
+rounds per puzzle, and a fixed workload for rocprofv3 --pmc passes.
+
+usage: python tools/solve_profile.py [--n N] [--workload solve17|solve30] [--reps R] [--stats]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_sudoku_solver_amd import SudokuEngine, synth, _lib as L  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=2_000_000)
+ap.add_argument("--workload", default="solve17")
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--stats", action="store_true")
+ap.add_argument("--waves-per-cu", type=int, default=0)
+args = ap.parse_args()
+
+gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
+p, s = gen(args.n, seed=11)
+with SudokuEngine(0) as eng:
+    if args.waves_per_cu:
+        eng.set_option(L.SDK_OPT_WAVES_PER_CU, args.waves_per_cu)
+    d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)
+    d_in.upload(p)
+    eng.solve_batch_dev(d_in, d_out, d_st, args.n)
+    eng.synchronize()
+    eng.timer_reset()
+    for _ in range(args.reps):
+        eng.solve_batch_dev(d_in, d_out, d_st, args.n)
+    eng.synchronize()
+    ms, nl = eng.timer_read()
+    out = np.empty((args.n, 81), np.uint8)
+    d_out.download(out)
+    print(f"{args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
+          f"ok={(out == s).all()}", flush=True)
+    if args.stats:
+        m = min(args.n, 200_000)
+        for kind, name in ((L.SDK_WORK_NODES, "nodes"), (L.SDK_WORK_ROUNDS, "rounds")):
+            eng.set_option(L.SDK_OPT_WORK_COUNTER, kind)
+            _, _, w = eng.solve_batch(p[:m], want_work=True)
+            print(f"{name}/puzzle: mean={w.mean():.2f} p50={np.median(w):.0f} p90={np.percentile(w, 90):.0f} "
+                  f"p99={np.percentile(w, 99):.0f} max={w.max()}", flush=True)
+        eng.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
+    for b in (d_in, d_out, d_st):
+        b.free()

@@ -30,6 +30,11 @@ SDK_OPT_WAVES_PER_CU = 3
 SDK_OPT_CHECK_BLOCKS_PER_CU = 4
 SDK_OPT_WORK_COUNTER = 5
 SDK_OPT_DEVICE_CUS = 6
+SDK_OPT_SOLVER = 7
+SDK_OPT_WAVES_PER_CU2 = 8
+
+SDK_SOLVER_WAVE = 0
+SDK_SOLVER_HALFWAVE = 1
 
 SDK_WORK_NODES = 0
 SDK_WORK_ROUNDS = 1

@@ -123,11 +123,15 @@ __device__ __forceinline__ void update_cell(uint32_t& x, uint32_t u, bool& bad, 
 //   [9..17]  digit of a given           -> duplicate givens make a unit non-exact
 //   [18..26] digit of a solved non-given -> duplicates are a conflict
 //   [27]     out-of-domain given        -> unit non-exact
+// (arithmetic only: early returns or ternaries over shifted values compile to
+// nested exec-mask blocks)
 __device__ __forceinline__ uint32_t contrib(uint32_t x) {
     const uint32_t v = x & kCands;
-    if (x & kInert) return 1u << 27;
-    if (x & kClue) return v | (v << 9);
-    return is_single(v) ? (v | (v << 18)) : v;
+    const uint32_t clue = (x >> 9) & 1u, inert = (x >> 10) & 1u;
+    const uint32_t single = (uint32_t)((v & (v - 1)) == 0);   // v == 0 contributes nothing either way
+    const uint32_t shift = 18u - 9u * clue;
+    const uint32_t r = v | ((v << shift) & (0u - (clue | single)));
+    return (r & (inert - 1u)) | (inert << 27);
 }
 
 __device__ __forceinline__ int propagate(const Wave& w, uint32_t& sa, uint32_t& sb, uint64_t& rounds) {
@@ -287,7 +291,8 @@ __device__ __forceinline__ void init_wave(Wave& w, uint32_t* s_cell, uint32_t* s
     }
 }
 
-__global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
+#ifndef SDK_NO_SOLVE_KERNEL   // solve2_launch.hip takes the helpers only
+__global__ __launch_bounds__(64, 8) void solve_kernel(SolveArgs a) {
     __shared__ uint32_t s_cell[96];
     __shared__ uint32_t s_unit[32];
     __shared__ uint32_t s_br[kMaxDepth];
@@ -348,5 +353,6 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
         }
     }
 }
+#endif  // SDK_NO_SOLVE_KERNEL
 
 }  // namespace sdk

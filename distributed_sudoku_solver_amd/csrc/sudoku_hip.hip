@@ -19,6 +19,11 @@
 #include "check_kernel.h"
 #include "solve_kernel.h"
 #include "frontier_kernel.h"
+#include "solve2_kernel.h"   // constants only: the kernel lives in solve2_launch.hip
+
+namespace sdk {
+hipError_t launch_solve2(const SolveArgs& a, unsigned grid, hipStream_t stream);
+}
 
 namespace {
 
@@ -60,6 +65,8 @@ struct sdk_ctx {
     int waves_per_cu = 32;
     int check_blocks_per_cu = 3;
     int work_rounds = 0;
+    int solver = SDK_SOLVER_HALFWAVE;
+    int waves_per_cu2 = 20;       // residency of solve2_kernel (LDS caps it at 20 per CU)
     // workspaces
     DevBuf stack, counter, in, mask, out, status, work, verdict;
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask;
@@ -122,13 +129,18 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
                  int order = -1) {
     if (n == 0) return SDK_OK;
     if (n > 0x7FFFFFFFull) return fail(SDK_EINVAL, "at most 2^31-1 boards per call");
-    const uint64_t slots = (uint64_t)c->cus * c->waves_per_cu;
-    // ~16 dequeues per wave over the launch, 1..64 boards each; count mode uses
-    // single boards (subtrees differ by orders of magnitude)
+    // two boards per wave (solve2_kernel) for solves; count mode stays one board per wave
+    const bool two = !count_mode && c->solver == SDK_SOLVER_HALFWAVE;
+    if (two && (!d_out || !d_status)) return fail(SDK_EINVAL, "solve needs out and status buffers");
+    const uint64_t slots = (uint64_t)c->cus * (two ? c->waves_per_cu2 : c->waves_per_cu) * (two ? 2 : 1);
+    // ~16 dequeues per board slot over the launch, 1..64 boards each; count mode
+    // uses single boards (subtrees differ by orders of magnitude)
     const uint32_t chunk = count_mode ? 1u : (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, n / (slots * 16)));
     const uint64_t want = (n + chunk - 1) / chunk;
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, slots));
-    int rc = ensure(c->stack, (size_t)grid * sdk::kStackWordsPerBlock * sizeof(uint32_t));
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(two ? (want + 1) / 2 : want,
+                                                                             two ? slots / 2 : slots));
+    const size_t stack_words = two ? sdk::kStack2WordsPerBlock : sdk::kStackWordsPerBlock;
+    int rc = ensure(c->stack, (size_t)grid * stack_words * sizeof(uint32_t));
     if (rc) return rc;
     rc = ensure(c->counter, 256);
     if (rc) return rc;
@@ -155,7 +167,11 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
     if (rc) return rc;
-    sdk::solve_kernel<<<grid, 64, 0, c->stream>>>(a);
+    if (two) {
+        HIPCALL(sdk::launch_solve2(a, grid, c->stream));
+    } else {
+        sdk::solve_kernel<<<grid, 64, 0, c->stream>>>(a);
+    }
     HIPCALL(hipGetLastError());
     HIPCALL(hipEventRecord(stop, c->stream));
     return SDK_OK;
@@ -398,6 +414,14 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             return SDK_OK;
         case SDK_OPT_DEVICE_CUS:
             return fail(SDK_EINVAL, "SDK_OPT_DEVICE_CUS is read-only");
+        case SDK_OPT_SOLVER:
+            if (value != SDK_SOLVER_WAVE && value != SDK_SOLVER_HALFWAVE) return fail(SDK_EINVAL, "bad solver %lld", (long long)value);
+            c->solver = (int)value;
+            return SDK_OK;
+        case SDK_OPT_WAVES_PER_CU2:
+            if (value < 1 || value > 32) return fail(SDK_EINVAL, "waves per CU must be 1..32");
+            c->waves_per_cu2 = (int)value;
+            return SDK_OK;
         default:
             return fail(SDK_EINVAL, "unknown option %d", key);
     }
@@ -413,6 +437,8 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_CHECK_BLOCKS_PER_CU: *value = c->check_blocks_per_cu; return SDK_OK;
         case SDK_OPT_WORK_COUNTER: *value = c->work_rounds; return SDK_OK;
         case SDK_OPT_DEVICE_CUS: *value = c->cus; return SDK_OK;
+        case SDK_OPT_SOLVER: *value = c->solver; return SDK_OK;
+        case SDK_OPT_WAVES_PER_CU2: *value = c->waves_per_cu2; return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }
 }

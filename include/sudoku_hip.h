@@ -68,6 +68,11 @@ extern "C" {
 #define SDK_OPT_CHECK_BLOCKS_PER_CU 4 /* checker grid = CUs x this, 1..16 (default 3)  */
 #define SDK_OPT_WORK_COUNTER 5  /* what solve `work` counts: SDK_WORK_* (default nodes) */
 #define SDK_OPT_DEVICE_CUS   6  /* read-only: compute units of the context's GPU        */
+#define SDK_OPT_SOLVER       7  /* solve kernel: SDK_SOLVER_* (default HALFWAVE)         */
+#define SDK_OPT_WAVES_PER_CU2 8 /* residency of the HALFWAVE solver, 1..32 (default 20) */
+
+#define SDK_SOLVER_WAVE      0  /* one board per wavefront (solve_kernel)              */
+#define SDK_SOLVER_HALFWAVE  1  /* two boards per wavefront, 27 lanes x 3 cells each   */
 
 #define SDK_WORK_NODES       0  /* search nodes (propagation fixpoints)                */
 #define SDK_WORK_ROUNDS      1  /* propagation rounds (profiling)                      */

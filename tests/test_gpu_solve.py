@@ -11,11 +11,25 @@ pytestmark = pytest.mark.gpu
 ORDERS = [L.SDK_ORDER_MRV_UNIQUE, L.SDK_ORDER_LEX]
 
 
-@pytest.fixture(params=ORDERS, ids=["mrv_unique", "lex"])
+SOLVERS = [L.SDK_SOLVER_HALFWAVE, L.SDK_SOLVER_WAVE]
+
+
+@pytest.fixture(params=[(s, o) for s in SOLVERS for o in ORDERS],
+                ids=["halfwave-mrv_unique", "halfwave-lex", "wave-mrv_unique", "wave-lex"])
 def ordered_engine(request, engine):
-    engine.set_option(L.SDK_OPT_ORDER, request.param)
+    solver, order = request.param
+    engine.set_option(L.SDK_OPT_SOLVER, solver)
+    engine.set_option(L.SDK_OPT_ORDER, order)
     yield engine
     engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE)
+
+
+@pytest.fixture(params=SOLVERS, ids=["halfwave", "wave"])
+def solver_engine(request, engine):
+    engine.set_option(L.SDK_OPT_SOLVER, request.param)
+    yield engine
+    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE)
 
 
 def test_golden_solve_cases(ordered_engine, solve_cases):
@@ -110,7 +124,8 @@ def test_conflicting_and_inert_givens_vs_oracle(ordered_engine):
     assert (out[done] == ref_out[done]).all()
 
 
-def test_17_clue_transforms_exact(engine):
+def test_17_clue_transforms_exact(solver_engine):
+    engine = solver_engine
     p, s = synth.make_17clue(20000, seed=99)
     out, st, work = engine.solve_batch(p, want_work=True)
     assert (st == 1).all()
@@ -118,13 +133,15 @@ def test_17_clue_transforms_exact(engine):
     assert (O.check_batch(out, 8) == 3).all()       # every output passes the reference check()
 
 
-def test_30_clue_exact(engine):
+def test_30_clue_exact(solver_engine):
+    engine = solver_engine
     p, s = synth.make_30clue(50000, seed=98)
     out, st, _ = engine.solve_batch(p)
     assert (st == 1).all() and (out == s).all()
 
 
-def test_lex_and_mrv_orders_agree_on_seeds(engine):
+def test_lex_and_mrv_orders_agree_on_seeds(solver_engine):
+    engine = solver_engine
     p, s = synth.seed_arrays()
     for order in ORDERS:
         engine.set_option(L.SDK_OPT_ORDER, order)
@@ -133,7 +150,8 @@ def test_lex_and_mrv_orders_agree_on_seeds(engine):
     engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
 
 
-def test_unsolvable_and_edge_boards(engine):
+def test_unsolvable_and_edge_boards(solver_engine):
+    engine = solver_engine
     boards = []
     b = np.zeros(81, np.uint8); b[0] = b[1] = 5              # '55' + 79 zeros: unsolvable, but no
     boards.append(b)                                           # singles-based refutation: budget hit
@@ -152,7 +170,8 @@ def test_unsolvable_and_edge_boards(engine):
     assert out[1].tolist() == ref[1]
 
 
-def test_budget_status(engine):
+def test_budget_status(solver_engine):
+    engine = solver_engine
     engine.set_option(L.SDK_OPT_NODE_BUDGET, 1)
     p, _ = synth.seed_arrays()
     b = np.zeros(81, np.uint8); b[0] = b[1] = 5
@@ -176,7 +195,8 @@ def test_count_solutions(engine):
         assert engine.count_solutions(b, limit=5000)[0] == O.count(b, 5000, 1)
 
 
-def test_empty_batch(engine):
+def test_empty_batch(solver_engine):
+    engine = solver_engine
     out, st, _ = engine.solve_batch(np.zeros((0, 81), np.uint8))
     assert out.shape == (0, 81) and st.shape == (0,)
 
@@ -267,3 +287,30 @@ def test_rccl_communicator_world1(engine):
         comm.close()
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 31, 33, 127, 1000])
+def test_ragged_batch_sizes(solver_engine, n):
+    """Odd sizes leave one half of a wave (HALFWAVE) or a chunk tail without a board."""
+    p, s = synth.make_17clue(n, seed=1000 + n)
+    out, st, _ = solver_engine.solve_batch(p)
+    assert (st == 1).all() and (out == s).all()
+
+
+def test_solvers_take_identical_search_paths(engine):
+    """Same propagation, same branching: per-board search nodes and propagation rounds agree."""
+    p, _ = synth.make_17clue(3000, seed=7)
+    sparse = _random_puzzles(300, 8, 18, 28)
+    boards = np.concatenate([p, sparse])
+    res = {}
+    for solver in SOLVERS:
+        engine.set_option(L.SDK_OPT_SOLVER, solver)
+        for kind in (L.SDK_WORK_NODES, L.SDK_WORK_ROUNDS):
+            engine.set_option(L.SDK_OPT_WORK_COUNTER, kind)
+            res[(solver, kind)] = engine.solve_batch(boards, want_work=True)
+    engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
+    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE)
+    for kind in (L.SDK_WORK_NODES, L.SDK_WORK_ROUNDS):
+        a, b = res[(SOLVERS[0], kind)], res[(SOLVERS[1], kind)]
+        assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
+        assert (a[2] == b[2]).all(), kind

@@ -18,13 +18,17 @@ ap.add_argument("--workload", default="solve17")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--stats", action="store_true")
 ap.add_argument("--waves-per-cu", type=int, default=0)
+ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave"])
+ap.add_argument("--sweep", action="store_true", help="time waves-per-CU settings")
 args = ap.parse_args()
 
 gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
 p, s = gen(args.n, seed=11)
 with SudokuEngine(0) as eng:
+    eng.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE if args.solver == "halfwave" else L.SDK_SOLVER_WAVE)
+    wopt = L.SDK_OPT_WAVES_PER_CU2 if args.solver == "halfwave" else L.SDK_OPT_WAVES_PER_CU
     if args.waves_per_cu:
-        eng.set_option(L.SDK_OPT_WAVES_PER_CU, args.waves_per_cu)
+        eng.set_option(wopt, args.waves_per_cu)
     d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)
     d_in.upload(p)
     eng.solve_batch_dev(d_in, d_out, d_st, args.n)
@@ -36,8 +40,18 @@ with SudokuEngine(0) as eng:
     ms, nl = eng.timer_read()
     out = np.empty((args.n, 81), np.uint8)
     d_out.download(out)
-    print(f"{args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
+    print(f"{args.solver} {args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
           f"ok={(out == s).all()}", flush=True)
+    if args.sweep:
+        for wpc in (8, 12, 16, 20, 24, 32):
+            eng.set_option(wopt, wpc)
+            eng.solve_batch_dev(d_in, d_out, d_st, args.n)
+            eng.synchronize()
+            eng.timer_reset()
+            eng.solve_batch_dev(d_in, d_out, d_st, args.n)
+            eng.synchronize()
+            ms, _ = eng.timer_read()
+            print(f"  {args.solver} waves/CU={wpc}: {ms:.3f} ms  {args.n / ms * 1e3 / 1e6:.1f} M/s", flush=True)
     if args.stats:
         m = min(args.n, 200_000)
         for kind, name in ((L.SDK_WORK_NODES, "nodes"), (L.SDK_WORK_ROUNDS, "rounds")):

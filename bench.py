@@ -43,6 +43,8 @@ def parse_args():
     ap.add_argument("--check-boards", type=int, default=100_000_000, help="checker boards per GPU (0 = skip)")
     ap.add_argument("--check-steps", type=int, default=10)
     ap.add_argument("--order", choices=["mrv_unique", "lex"], default="mrv_unique")
+    ap.add_argument("--solver", choices=["halfwave", "wave"], default="halfwave",
+                    help="solve kernel: two boards per wave (solve2_kernel) or one (solve_kernel)")
     ap.add_argument("--waves-per-cu", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -131,6 +133,34 @@ def cpu_baseline(puzzles, seconds, threads):
     }
 
 
+def cpu_baseline_python(puzzles, seconds, procs):
+    """The oracle's line-by-line Python restatement of DHTNode.solve_sudoku
+    (oracle.py_naive_solve, DHT_Node.py:474-538) -- the closest stand-in for the
+    reference's own Python solver, which cannot travel to the GPU box -- one process
+    per core (like one DHT node per core), each on its own slice of the batch."""
+    import multiprocessing as mp
+    from oracle import oracle as O
+    per = max(1, int(seconds / 0.01))          # more than a process can finish
+    slices = [[list(map(int, puzzles[i])) for i in range(k * per, min((k + 1) * per, len(puzzles)))]
+              for k in range(procs)]
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.starmap(O.py_solve_timed, [(sl, seconds) for sl in slices])
+    wall = time.perf_counter() - t0
+    done = sum(r[0] for r in res)
+    solved = sum(r[1] for r in res)
+    busy = max(r[2] for r in res)
+    return {
+        "value": solved / busy if busy > 0 else 0.0,
+        "unit": "puzzles/s",
+        "cores": procs,
+        "kind": "port",
+        "sample": (f"{done} puzzles of the rank-0 batch ({procs} disjoint slices), pure-Python naive DFS "
+                   f"(oracle/oracle.py py_naive_solve, restates DHT_Node.py:474-538 line by line), "
+                   f"{procs} processes, {busy:.1f} s solving ({wall:.1f} s incl. process start)"),
+    }
+
+
 def c2_leg(eng, d, args, synth):
     """Config C2: ~30-clue unique puzzles, resident in HBM, one launch per step."""
     n = args.c2_puzzles
@@ -161,11 +191,12 @@ def c2_leg(eng, d, args, synth):
            "value": d.world * n * steps / el, "unit": "puzzles/s", "avg_kernel_ms": k_s * 1000.0,
            "roofline": {"bound": "hbm", "achieved": SOLVE_BYTES_PER_PUZZLE * n / k_s / 1e9, "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": SOLVE_BYTES_PER_PUZZLE * n / k_s / 1e9 / HBM_PEAK_GBPS,
-                        "kernel": "sdk::solve_kernel"},
+                        "kernel": args.solve_kernel},
            "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
-        leg["cpu_baseline"] = cpu_baseline(p, min(5.0, args.cpu_seconds),
-                                           max(1, min(args.cpu_threads, os.cpu_count() or 1)))
+        cores = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        leg["cpu_baseline"] = cpu_baseline(p, min(5.0, args.cpu_seconds), cores)
+        leg["cpu_baseline_python"] = cpu_baseline_python(p, min(5.0, args.cpu_seconds), cores)
     return leg
 
 
@@ -233,8 +264,12 @@ def main():
 
     eng = SudokuEngine(d.local_rank)
     eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
+    eng.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE if args.solver == "halfwave" else L.SDK_SOLVER_WAVE)
     if args.waves_per_cu:
-        eng.set_option(L.SDK_OPT_WAVES_PER_CU, args.waves_per_cu)
+        eng.set_option(L.SDK_OPT_WAVES_PER_CU2 if args.solver == "halfwave" else L.SDK_OPT_WAVES_PER_CU,
+                       args.waves_per_cu)
+    solve_kernel = "sdk::solve2_kernel" if args.solver == "halfwave" else "sdk::solve_kernel"
+    args.solve_kernel = solve_kernel
 
     # ---------------------------------------------------------------- solve
     n = args.batch
@@ -302,9 +337,9 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             # the committed PMC passes ran this bench at its default sizes
-            "traffic": pmc_traffic(args.pmc_summary, "sdk::solve_kernel") if n == 10_000_000 else None,
+            "traffic": pmc_traffic(args.pmc_summary, solve_kernel) if n == 10_000_000 else None,
             "traffic_source": args.pmc_summary and os.path.relpath(args.pmc_summary, ROOT),
-            "kernel": "sdk::solve_kernel",
+            "kernel": solve_kernel,
             "avg_kernel_ms": avg_kernel_s * 1000.0,
             "note": "search is VALU/LDS-latency bound; HBM fraction reported per contract",
         },

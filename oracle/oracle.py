@@ -170,3 +170,19 @@ def py_check(cells):
     box00_sum = sum(g[k][l] for k in range(3) for l in range(3))
     raw = "NameError" if (rows and cols and box00_sum == 45) else "False"
     return raw, bool(boxes)
+
+
+def py_solve_timed(boards, seconds):
+    """Baseline worker (bench.py cpu_baseline leg): the Python restatement above on
+    `boards` (list of 81-int lists) one after another until `seconds` have passed.
+    Returns (done, solved, wall_s)."""
+    import time
+    t0 = time.perf_counter()
+    done = solved = 0
+    for cells in boards:
+        if time.perf_counter() - t0 >= seconds:
+            break
+        ok, _, _ = py_naive_solve(cells)
+        done += 1
+        solved += int(ok)
+    return done, solved, time.perf_counter() - t0

@@ -18,7 +18,27 @@
 // completions, node count, board index) lives in VGPRs, identical across the
 // half's lanes.
 //
-// DFS stack: one 8-byte snapshot (the lane's three 16-bit cell states) per lane
+// Cell state = its contribution word.  solve_kernel keeps 16-bit states and
+// converts each to the bit-sliced contribution word (solve_kernel.h contrib())
+// before every LDS write; here the state IS that word, so the three writes of a
+// round need no VALU work and only a cell that changes pays for the format:
+//   [0..8]   candidates
+//   [9..17]  the digit of a given (1..9)
+//   [18..26] the digit of a solved non-given cell (set iff one candidate is left)
+//   [27]     out-of-domain given (10..255): constrains nothing
+// so  open (branchable) <=> state < 0x200 with >= 2 candidates, and a
+// contradiction cell (no candidate) is the state 0.
+//
+// Bank-conflict-free unit reads: read k of a unit lane fetches the cell of its
+// unit that holds digit k+1 in the fixed Sudoku solution
+// G(r,c) = (3(r%3) + 2(r/3) + c) mod 9.  The 9 cells of one digit of a solution
+// are one per row, column and box, so in every read the 27 lanes of a half
+// fetch only 9 distinct words (each broadcast to its row, column and box lane),
+// and for this G those 9 words sit in 9 distinct banks of ds_read_b32's
+// 32-lane group (tools/lds_banks.py checks it).  Spare lanes 27..31 read what
+// lane 0 of their half reads.
+//
+// DFS stack: one 8-byte snapshot (the lane's three cell states, packed to 16 bits) per lane
 // per level; the first kLdsLevels levels are LDS-resident, deeper levels go to a
 // per-workgroup HBM region (L2-resident).  Branch records (cell, untried digits)
 // are in LDS.  Count mode (frontier counts) stays on solve_kernel.
@@ -68,15 +88,17 @@ __device__ __forceinline__ void init_lane2(Lane2& w, uint32_t* s_cell_all, uint3
         w.c2 = 91 + e;
         w.ucol = w.ur0 = w.ur1 = w.ur2 = w.ub0 = w.ub1 = w.ub2 = 27 + e;
     }
+    // unit j's cell holding digit k+1 of G (see the header); spare lanes copy lane 0
+    const int uj = w.act ? j : 0;
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
-        int cell;
-        if (!w.act) cell = 81 + k;
-        else if (j < 9) cell = 9 * j + k;
-        else if (j < 18) cell = 9 * k + (j - 9);
-        else {
-            const int b = j - 18;
-            cell = ((b / 3) * 3 + k / 3) * 9 + (b % 3) * 3 + k % 3;
+        int cell = 0;
+        for (int q = 0; q < 9; ++q) {
+            int r, c;
+            if (uj < 9) { r = uj; c = q; }
+            else if (uj < 18) { r = q; c = uj - 9; }
+            else { r = ((uj - 18) / 3) * 3 + q / 3; c = ((uj - 18) % 3) * 3 + q % 3; }
+            if ((3 * (r % 3) + 2 * (r / 3) + c) % 9 == k) cell = 9 * r + c;
         }
         w.ucell[k] = cell;
     }
@@ -91,6 +113,15 @@ __device__ __forceinline__ bool half_any(const Lane2& w, bool pred) {
     return (w.half ? hi : lo) != 0u;
 }
 
+// per-half vote on a lane mask, all scalar: a lane's result is whether any lane of
+// its half has `pred` (inverse_ballot turns the uniform mask back into lane bools)
+__device__ __forceinline__ bool half_any_s(bool pred) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(pred);
+    const uint64_t lo = (__builtin_amdgcn_readfirstlane((int)m) != 0) ? 0x00000000FFFFFFFFull : 0ull;
+    const uint64_t hi = (__builtin_amdgcn_readfirstlane((int)(m >> 32)) != 0) ? 0xFFFFFFFF00000000ull : 0ull;
+    return __builtin_amdgcn_inverse_ballot_w64(lo | hi);
+}
+
 // min over the 32 lanes of each half (all lanes of the half must be active)
 __device__ __forceinline__ uint32_t half_min(uint32_t v) {
 #pragma unroll
@@ -103,29 +134,57 @@ __device__ __forceinline__ uint32_t half_first(const Lane2& w, uint32_t v) {
     return (uint32_t)__shfl((int)v, w.half * 32);
 }
 
-// update_cell (solve_kernel.h) as a branch-free value function: three guarded
-// in-place updates of s0/s1/s2 get merged into one store through a phi of their
-// addresses, which demotes the cells to scratch memory.
+constexpr uint32_t kGiven2 = 0x3FE00u;      // [9..17] digit of a given
+constexpr uint32_t kInert2 = 1u << 27;      // out-of-domain given
+constexpr uint32_t kOpenLimit2 = 0x200u;    // states below this are non-given, unsolved (or empty)
+
+// state of input byte v (0 = empty)
+__device__ __forceinline__ uint32_t cell_init2(uint32_t v) {
+    const uint32_t m = 1u << ((v - 1u) & 31u);
+    return v == 0 ? kCands : (v <= 9 ? (m | (m << 9)) : kInert2);
+}
+
+// state of a non-given cell with candidates v: the solved field is set iff one is left
+__device__ __forceinline__ uint32_t norm2(uint32_t v) {
+    return v | (((v & (v - 1u)) == 0u) ? (v << 18) : 0u);
+}
+
+// 16-bit snapshot form (candidates | given << 9 | inert << 10) and back
+__device__ __forceinline__ uint32_t pack2(uint32_t x) {
+    return (x & kCands) | ((x & kGiven2) ? 0x200u : 0u) | ((x >> 27) << 10);
+}
+__device__ __forceinline__ uint32_t unpack2(uint32_t y) {
+    const uint32_t v = y & kCands;
+    return (y & 0x400u) ? kInert2 : ((y & 0x200u) ? (v | (v << 9)) : norm2(v));
+}
+
+// branchable cell: candidate count, else 0
+__device__ __forceinline__ uint32_t open_count2(uint32_t x) {
+    return x < kOpenLimit2 ? (uint32_t)__popc(x) : 0u;
+}
+
+// update_cell (solve_kernel.h) on the contribution-format state, as a branch-free
+// value function: three guarded in-place updates of s0/s1/s2 get merged into one
+// store through a phi of their addresses, which demotes the cells to scratch memory.
 __device__ __forceinline__ uint32_t updated_cell(uint32_t x, uint32_t u, bool& bad, bool& chg) {
-    const uint32_t v = x & kCands;
-    const bool fixed = (x & kFixed) != 0;
-    const bool open = !fixed & ((v & (v - 1)) != 0);
-    const uint32_t v1 = v & ~u;
-    const uint32_t h = v1 & (u >> 16) & kCands;
+    // every state below 0x200 is an empty cell with >= 2 candidates, or 0
+    const bool open = (x - 1u) < kOpenLimit2 - 1u;
+    const uint32_t v1 = x & ~u;                 // (only meaningful when open: then x = candidates)
+    const uint32_t h = v1 & (u >> 16);          // u >> 16 = hidden-single digits (9 bits)
     const uint32_t v2 = h ? h : v1;
-    bad |= (open & (((h & (h - 1)) != 0) | (v2 == 0))) | (!fixed & (v == 0));
-    const bool c = open & (v2 != v);
-    chg |= c;
-    return c ? v2 : x;
+    bad |= (open & (((h & (h - 1u)) != 0u) | (v2 == 0u))) | (x == 0u);
+    const uint32_t n = open ? norm2(v2) : x;
+    chg |= n != x;
+    return n;
 }
 
 // One propagation round for both halves, branch-free (idle lanes work on spare
 // slots).  Per lane: bad (contradiction in MY half), chg (a cell of MY half changed).
 __device__ __forceinline__ void round2(const Lane2& w, uint32_t& s0, uint32_t& s1, uint32_t& s2, bool& bad,
                                        bool& chg) {
-    w.s_cell[w.c0] = contrib(s0);
-    w.s_cell[w.c1] = contrib(s1);
-    w.s_cell[w.c2] = contrib(s2);
+    w.s_cell[w.c0] = s0;
+    w.s_cell[w.c1] = s1;
+    w.s_cell[w.c2] = s2;
     __syncthreads();
     uint32_t ones = 0, twos = 0;
 #pragma unroll
@@ -147,14 +206,14 @@ __device__ __forceinline__ void round2(const Lane2& w, uint32_t& s0, uint32_t& s
     s0 = updated_cell(s0, uc | w.s_unit[w.ur0] | w.s_unit[w.ub0], b, c);
     s1 = updated_cell(s1, uc | w.s_unit[w.ur1] | w.s_unit[w.ub1], b, c);
     s2 = updated_cell(s2, uc | w.s_unit[w.ur2] | w.s_unit[w.ub2], b, c);
-    bad = half_any(w, b);
-    chg = half_any(w, c);
+    bad = half_any_s(b);
+    chg = half_any_s(c);
 }
 
 // branch key of a cell: (candidates << 16 | cell << 9 | mask) for MRV, (cell << 9 | mask)
 // for LEX; ~0 for cells that are not branchable
 __device__ __forceinline__ uint32_t branch_key(uint32_t x, int cell, int order) {
-    const uint32_t k = open_count(x);
+    const uint32_t k = open_count2(x);
     if (k < 2) return ~0u;
     const uint32_t base = ((uint32_t)cell << 9) | (x & kCands);
     return order == ORDER_LEX ? base : (k << 16) | base;
@@ -162,6 +221,7 @@ __device__ __forceinline__ uint32_t branch_key(uint32_t x, int cell, int order) 
 
 __device__ __forceinline__ void set_cell2(const Lane2& w, uint32_t& s0, uint32_t& s1, uint32_t& s2, int cell,
                                           uint32_t d) {
+    d |= d << 18;
     s0 = (w.act && cell == w.c0) ? d : s0;
     s1 = (w.act && cell == w.c1) ? d : s1;
     s2 = (w.act && cell == w.c2) ? d : s2;
@@ -207,9 +267,9 @@ __device__ __forceinline__ void start_board(const Lane2& w, const Args2& a, Boar
         b.in1 = w.act ? (uint32_t)src[w.c1] : 0u;
         b.in2 = w.act ? (uint32_t)src[w.c2] : 0u;
     }
-    b.s0 = w.act ? cell_init(b.in0) : kInert;
-    b.s1 = w.act ? cell_init(b.in1) : kInert;
-    b.s2 = w.act ? cell_init(b.in2) : kInert;
+    b.s0 = w.act ? cell_init2(b.in0) : kInert2;
+    b.s1 = w.act ? cell_init2(b.in1) : kInert2;
+    b.s2 = w.act ? cell_init2(b.in2) : kInert2;
     if (a.mask) {
         // TASK `range` restricts the lowest-index empty input cell only (DHT_Node.py:474,522,531)
         const uint32_t fm = ((uint32_t)a.mask[b.bidx] >> 1) & kCands;
@@ -219,10 +279,11 @@ __device__ __forceinline__ void start_board(const Lane2& w, const Args2& a, Boar
         z = half_min(z);
         // branch-free: guarded stores to different cells would be merged into one
         // store through a phi of addresses, which demotes the cells to scratch
-        const uint32_t keep = fm | ~kCands;
-        b.s0 = (w.act && z == (uint32_t)w.c0) ? (b.s0 & keep) : b.s0;
-        b.s1 = (w.act && z == (uint32_t)w.c1) ? (b.s1 & keep) : b.s1;
-        b.s2 = (w.act && z == (uint32_t)w.c2) ? (b.s2 & keep) : b.s2;
+        // (that cell is empty: its state is kCands, restricted to norm2(fm))
+        const uint32_t ms = norm2(fm);
+        b.s0 = (w.act && z == (uint32_t)w.c0) ? ms : b.s0;
+        b.s1 = (w.act && z == (uint32_t)w.c1) ? ms : b.s1;
+        b.s2 = (w.act && z == (uint32_t)w.c2) ? ms : b.s2;
     }
     b.depth = 0;
     b.count = 0;
@@ -243,7 +304,7 @@ __device__ __forceinline__ void next_board(const Lane2& w, const Args2& a, Board
     b.lim = b.order == ORDER_LEX ? 1u : 2u;
     b.nodes = b.rounds = 0;
     if (b.active) start_board(w, a, b, true);
-    else b.s0 = b.s1 = b.s2 = kInert;
+    else b.s0 = b.s1 = b.s2 = kInert2;
 }
 
 __device__ __forceinline__ void finish_board(const Lane2& w, const Args2& a, Board2& b, int st) {
@@ -302,7 +363,7 @@ __global__ __launch_bounds__(64) void solve2_kernel(SolveArgs args) {
         if (!ev) continue;
         ++b.nodes;
         int r = bad ? P_CONTRA
-                    : (half_any(w, open_count(b.s0) >= 2 || open_count(b.s1) >= 2 || open_count(b.s2) >= 2) ? P_OPEN
+                    : (half_any(w, open_count2(b.s0) >= 2 || open_count2(b.s1) >= 2 || open_count2(b.s2) >= 2) ? P_OPEN
                                                                                                           : P_SOLVED);
         if (a.budget && b.nodes > a.budget) {
             finish_board(w, a, b, -2);
@@ -337,7 +398,7 @@ __global__ __launch_bounds__(64) void solve2_kernel(SolveArgs args) {
             const int cell = (int)((key >> 9) & 0x7Fu);
             const uint32_t m = key & kCands;
             const uint32_t d = m & (0u - m);
-            const uint2 snap = make_uint2(b.s0 | (b.s1 << 16), b.s2);
+            const uint2 snap = make_uint2(pack2(b.s0) | (pack2(b.s1) << 16), pack2(b.s2));
             if (b.depth < kLdsLevels) s_stk[b.depth][w.lane] = snap;
             else g_stk[b.depth * 64 + w.lane] = snap;
             if (w.hl == 0) s_br[w.half][b.depth] = (uint32_t)cell | ((m ^ d) << 16);
@@ -356,9 +417,9 @@ __global__ __launch_bounds__(64) void solve2_kernel(SolveArgs args) {
         const uint32_t d = rest & (0u - rest);
         rest ^= d;
         const uint2 snap = b.depth - 1 < kLdsLevels ? s_stk[b.depth - 1][w.lane] : g_stk[(b.depth - 1) * 64 + w.lane];
-        b.s0 = snap.x & 0xFFFFu;
-        b.s1 = snap.x >> 16;
-        b.s2 = snap.y;
+        b.s0 = unpack2(snap.x & 0xFFFFu);
+        b.s1 = unpack2(snap.x >> 16);
+        b.s2 = unpack2(snap.y);
         if (rest == 0) --b.depth;
         else if (w.hl == 0) s_br[w.half][b.depth - 1] = (uint32_t)cell | (rest << 16);
         set_cell2(w, b.s0, b.s1, b.s2, cell, d);

@@ -10,14 +10,14 @@ import sys
 from collections import defaultdict
 
 
-def main(d):
+def main(d, all_kernels=False):
     vals = defaultdict(lambda: defaultdict(float))
     ndisp = defaultdict(set)
     for f in sorted(glob.glob(os.path.join(d, "pass*", "**", "*counter_collection.csv"), recursive=True)):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"].split("(")[0]
-                if not k.startswith("sdk::"):
+                if not all_kernels and not k.startswith("sdk::"):
                     continue
                 vals[k][row["Counter_Name"]] += float(row["Counter_Value"])
                 ndisp[k].add((f, row["Dispatch_Id"]))
@@ -37,4 +37,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], "--all" in sys.argv[2:])

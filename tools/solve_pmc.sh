@@ -11,6 +11,7 @@ cat "$out/solve_stats.txt"
 i=0
 for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS" \
             "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_INSTS_BRANCH" \
+            "SQ_LDS_IDX_ACTIVE SQ_BUSY_CU_CYCLES SQ_INST_CYCLES_VALU SQ_INSTS_VALU_INT32" \
             "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $pass --output-format csv -d "$root/$out/pass$i" -o run -- \

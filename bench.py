@@ -42,6 +42,8 @@ def parse_args():
     ap.add_argument("--batch", type=int, default=10_000_000, help="puzzles per GPU")
     ap.add_argument("--check-boards", type=int, default=100_000_000, help="checker boards per GPU (0 = skip)")
     ap.add_argument("--check-steps", type=int, default=10)
+    ap.add_argument("--check-warmup", type=int, default=10,
+                    help="untimed checker launches first (the memory clocks ramp under sustained streaming)")
     ap.add_argument("--order", choices=["mrv_unique", "lex"], default="mrv_unique")
     ap.add_argument("--solver", choices=["halfwave", "wave"], default="halfwave",
                     help="solve kernel: two boards per wave (solve2_kernel) or one (solve_kernel)")
@@ -271,6 +273,57 @@ def main():
     solve_kernel = "sdk::solve2_kernel" if args.solver == "halfwave" else "sdk::solve_kernel"
     args.solve_kernel = solve_kernel
 
+    # -------------------------------------------------------------- checker
+    # Runs before the solver leg, on a fresh allocation: measured after the solver leg the same
+    # kernel read ~9% slower on the same box (profiles/r01/check_variants.txt).
+    checker_leg = None
+    if args.check_boards > 0:
+        nb = args.check_boards
+        pool_n = min(nb, 1 << 20)
+        pool, pool_exp = synth.make_check_boards(pool_n, seed=args.seed + 7 + 1000 * d.rank)
+        d_b = eng.alloc(nb * 81)
+        d_v = eng.alloc(nb)
+        # tile the pool through HBM (content repeats; every byte is still streamed from HBM)
+        import ctypes
+        for s in range(0, nb, pool_n):
+            m = min(pool_n, nb - s)
+            L.check(eng.lib.sdk_memcpy_h2d(eng.ctx, ctypes.c_void_p(d_b.ptr.value + s * 81),
+                                           ctypes.c_void_p(pool.ctypes.data), m * 81), "h2d")
+        for _ in range(max(1, args.check_warmup)):
+            eng.check_batch_dev(d_b, d_v, nb)
+        eng.synchronize()
+        eng.timer_reset()
+        d.barrier()
+        eng.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.check_steps):
+            eng.check_batch_dev(d_b, d_v, nb)
+        eng.synchronize()
+        d.barrier()
+        cel = d.max(time.perf_counter() - t0)
+        cms, cl = eng.timer_read()
+        v = np.empty(nb, np.uint8)
+        d_v.download(v)
+        reps = (nb + pool_n - 1) // pool_n
+        exp = np.tile(pool_exp, reps)[:nb]
+        cbad = int(d.sum(int((v != exp).sum())))
+        d_b.free()
+        d_v.free()
+        ck_s = cms / 1000.0 / max(cl, 1)
+        ach = CHECK_BYTES_PER_BOARD * nb / ck_s / 1e9
+        checker_leg = {
+            "workload": f"C3: {nb} complete boards per GPU (50% valid), literal sudoku.py:43-94 rule",
+            "value": d.world * nb * args.check_steps / cel,
+            "unit": "boards/s",
+            "avg_kernel_ms": ck_s * 1000.0,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBPS,
+                         "traffic": pmc_traffic(args.pmc_summary, "sdk::check_kernel")
+                         if nb == 100_000_000 else None,
+                         "kernel": "sdk::check_kernel"},
+            "parity": {"mismatched_boards": cbad, "checked_boards": d.world * nb},
+        }
+
     # ---------------------------------------------------------------- solve
     n = args.batch
     gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
@@ -346,52 +399,8 @@ def main():
         "parity": {"mismatched_boards": bad_total, "checked_boards": d.world * n},
     }
 
-    # -------------------------------------------------------------- checker
-    if args.check_boards > 0:
-        nb = args.check_boards
-        pool_n = min(nb, 1 << 20)
-        pool, pool_exp = synth.make_check_boards(pool_n, seed=args.seed + 7 + 1000 * d.rank)
-        d_b = eng.alloc(nb * 81)
-        d_v = eng.alloc(nb)
-        # tile the pool through HBM (content repeats; every byte is still streamed from HBM)
-        import ctypes
-        for s in range(0, nb, pool_n):
-            m = min(pool_n, nb - s)
-            L.check(eng.lib.sdk_memcpy_h2d(eng.ctx, ctypes.c_void_p(d_b.ptr.value + s * 81),
-                                           ctypes.c_void_p(pool.ctypes.data), m * 81), "h2d")
-        eng.check_batch_dev(d_b, d_v, nb)
-        eng.synchronize()
-        eng.timer_reset()
-        d.barrier()
-        eng.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.check_steps):
-            eng.check_batch_dev(d_b, d_v, nb)
-        eng.synchronize()
-        d.barrier()
-        cel = d.max(time.perf_counter() - t0)
-        cms, cl = eng.timer_read()
-        v = np.empty(nb, np.uint8)
-        d_v.download(v)
-        reps = (nb + pool_n - 1) // pool_n
-        exp = np.tile(pool_exp, reps)[:nb]
-        cbad = int(d.sum(int((v != exp).sum())))
-        d_b.free()
-        d_v.free()
-        ck_s = cms / 1000.0 / max(cl, 1)
-        ach = CHECK_BYTES_PER_BOARD * nb / ck_s / 1e9
-        result["checker"] = {
-            "workload": f"C3: {nb} complete boards per GPU (50% valid), literal sudoku.py:43-94 rule",
-            "value": d.world * nb * args.check_steps / cel,
-            "unit": "boards/s",
-            "avg_kernel_ms": ck_s * 1000.0,
-            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBPS,
-                         "traffic": pmc_traffic(args.pmc_summary, "sdk::check_kernel")
-                         if nb == 100_000_000 else None,
-                         "kernel": "sdk::check_kernel"},
-            "parity": {"mismatched_boards": cbad, "checked_boards": d.world * nb},
-        }
+    if checker_leg is not None:
+        result["checker"] = checker_leg
 
     # side legs run under a watchdog: if one stalls (e.g. a collective), rank 0
     # still prints the line with everything measured so far

@@ -32,6 +32,12 @@ SDK_OPT_WORK_COUNTER = 5
 SDK_OPT_DEVICE_CUS = 6
 SDK_OPT_SOLVER = 7
 SDK_OPT_WAVES_PER_CU2 = 8
+SDK_OPT_CHECK_VARIANT = 9
+SDK_CHECK_REG1 = 0
+SDK_CHECK_REG2 = 1
+SDK_CHECK_GLDS2 = 2
+SDK_CHECK_GLDS3 = 3
+SDK_CHECK_GLDS4 = 4
 
 SDK_SOLVER_WAVE = 0
 SDK_SOLVER_HALFWAVE = 1

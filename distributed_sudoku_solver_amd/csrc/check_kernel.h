@@ -145,4 +145,137 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel(const uint8_t* __r
     }
 }
 
+// Variant: two tiles in flight per workgroup (register ring of depth 2, the loop
+// unrolled by two so the ring index stays compile-time and the ring in VGPRs).
+__global__ __launch_bounds__(kCheckThreads) void check_kernel_rr2(const uint8_t* __restrict__ boards,
+                                                                  uint8_t* __restrict__ verdict, uint64_t n) {
+    __shared__ __attribute__((aligned(16))) u32x4 tile[kCheckTileVec + 1];
+    constexpr int kFull = kCheckTileVec / kCheckThreads;
+    constexpr int kRem = kCheckTileVec % kCheckThreads;
+    const int t = threadIdx.x;
+    const uint64_t nfull = n / kCheckThreads;
+    const uint64_t ntiles = (n + kCheckThreads - 1) / kCheckThreads;
+    const uint64_t G = gridDim.x;
+    u32x4 ra[kFull + 1], rb[kFull + 1];
+    // Loads are issued unconditionally (past-the-end tiles clamp to the last full
+    // tile, lanes >= kRem re-read lane t % kRem's vector): with no branch around
+    // them the compiler's vmcnt waits stay counted and the other ring slot stays in
+    // flight. Requires nfull >= 1 (the launcher uses check_kernel for tiny n).
+    auto load_tile = [&](uint64_t ti, u32x4 (&pre)[kFull + 1]) {
+        ti = min(ti, nfull - 1);
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(boards + ti * kCheckTileBytes);
+#pragma unroll
+        for (int j = 0; j < kFull; ++j) pre[j] = __builtin_nontemporal_load(&s4[j * kCheckThreads + t]);
+        pre[kFull] = __builtin_nontemporal_load(&s4[kFull * kCheckThreads + (t & (kRem - 1))]);
+    };
+    // cur holds tile tix (if full), nxt holds tile tix + G in flight
+    auto step = [&](uint64_t tix, u32x4 (&cur)[kFull + 1]) {
+        const uint64_t base = tix * kCheckThreads;
+        const uint64_t cnt = min((uint64_t)kCheckThreads, n - base);
+        if (cnt == (uint64_t)kCheckThreads) {
+#pragma unroll
+            for (int j = 0; j < kFull; ++j) tile[j * kCheckThreads + t] = cur[j];
+            if (t < kRem) tile[kFull * kCheckThreads + t] = cur[kFull];
+        } else {
+            const uint8_t* src = boards + base * 81;
+            uint8_t* tb = reinterpret_cast<uint8_t*>(tile);
+            if ((uint64_t)t < cnt) {
+#pragma unroll
+                for (int k = 0; k < 81; ++k) tb[81 * t + k] = src[81 * t + k];
+            }
+        }
+        __syncthreads();
+        load_tile(tix + 2 * G, cur);
+        if ((uint64_t)t < cnt)
+            verdict[base + t] = check_board_lds(reinterpret_cast<const uint32_t*>(tile), t);
+        __syncthreads();
+    };
+    uint64_t tix = blockIdx.x;
+    load_tile(tix, ra);
+    load_tile(tix + G, rb);
+    // The scheduler interleaves the two prologue tiles; left pending, that order
+    // would make the loop's merged waits drain both slots. Drain once here instead.
+    __builtin_amdgcn_s_waitcnt(0);
+    for (; tix < ntiles; tix += 2 * G) {
+        step(tix, ra);
+        if (tix + G >= ntiles) break;
+        step(tix + G, rb);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Variant: LDS-DMA ring. NBUF tile buffers in ONE __shared__ array; tiles are
+// fetched HBM -> LDS with global_load_lds_dwordx4 (no VGPR staging, lane-linear
+// 1 KiB per wave-instruction), NBUF-1 tiles ahead. Counted vmcnt + raw s_barrier
+// keep the later tiles in flight across the barriers (a __syncthreads() would
+// drain them). Global stores share the VM counter but are never counted in the
+// wait: waiting for <= D*G loads outstanding retires every load of the current
+// tile whatever the stores do, because loads retire in order.
+template <int NBUF>
+__global__ __launch_bounds__(kCheckThreads) void check_kernel_glds(const uint8_t* __restrict__ boards,
+                                                                   uint8_t* __restrict__ verdict, uint64_t n) {
+    __shared__ __attribute__((aligned(16))) u32x4 ring[NBUF * kCheckTileVec + 1];
+    constexpr int D = NBUF - 1;
+    constexpr int kFull = kCheckTileVec / kCheckThreads;   // 5 glds per wave per tile
+    constexpr int kRem = kCheckTileVec % kCheckThreads;    // wave 0: a 6th for 16 lanes
+    const int t = threadIdx.x;
+    const int wave = t >> 6;
+    const uint64_t nfull = n / kCheckThreads;
+    const uint64_t ntiles = (n + kCheckThreads - 1) / kCheckThreads;
+    const uint64_t G = gridDim.x;
+    auto issue = [&](uint64_t ti, int buf) {
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(boards + ti * kCheckTileBytes);
+        u32x4* d = ring + buf * kCheckTileVec;
+#pragma unroll
+        for (int j = 0; j < kFull; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)&s4[j * kCheckThreads + t],
+                                             (__attribute__((address_space(3))) void*)(d + j * kCheckThreads + wave * 64),
+                                             16, 0, 2);
+        if (t < kRem)
+            __builtin_amdgcn_global_load_lds((const void*)&s4[kFull * kCheckThreads + t],
+                                             (__attribute__((address_space(3))) void*)(d + kFull * kCheckThreads),
+                                             16, 0, 2);
+    };
+    uint64_t tix = blockIdx.x;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if (tix + d * G < nfull) issue(tix + d * G, d);
+    int buf = 0;
+    for (; tix < ntiles; tix += G) {
+        const uint64_t ahead = tix + D * G;
+        const uint64_t base = tix * kCheckThreads;
+        const uint64_t cnt = min((uint64_t)kCheckThreads, n - base);
+        u32x4* cur = ring + buf * kCheckTileVec;
+        if (ahead < nfull) {
+            int nb = buf + D;
+            if (nb >= NBUF) nb -= NBUF;
+            issue(ahead, nb);
+            if (wave == 0) wait_vmcnt<D*(kFull + 1)>();
+            else wait_vmcnt<D * kFull>();
+        } else {
+            wait_vmcnt<0>();
+            if (cnt != (uint64_t)kCheckThreads) {
+                const uint8_t* src = boards + base * 81;
+                uint8_t* tb = reinterpret_cast<uint8_t*>(cur);
+                if ((uint64_t)t < cnt) {
+#pragma unroll
+                    for (int k = 0; k < 81; ++k) tb[81 * t + k] = src[81 * t + k];
+                }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's ds_writes (ragged path) landed
+        __builtin_amdgcn_s_barrier();
+        if ((uint64_t)t < cnt)
+            verdict[base + t] = check_board_lds(reinterpret_cast<const uint32_t*>(cur), t);
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // this wave's ds_reads of cur are done
+        __builtin_amdgcn_s_barrier();         // nobody reads cur when the next iteration refills it
+        buf = (buf + 1 == NBUF) ? 0 : buf + 1;
+    }
+    wait_vmcnt<0>();
+}
+
 }  // namespace sdk

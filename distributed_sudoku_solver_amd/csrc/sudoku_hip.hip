@@ -64,6 +64,7 @@ struct sdk_ctx {
     uint64_t budget = 0;
     int waves_per_cu = 32;
     int check_blocks_per_cu = 3;
+    int check_variant = SDK_CHECK_REG1;
     int work_rounds = 0;
     int solver = SDK_SOLVER_HALFWAVE;
     int waves_per_cu2 = 20;       // residency of solve2_kernel (LDS caps it at 20 per CU)
@@ -117,7 +118,15 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
     hipEvent_t stop;
     int rc = timer_begin(c, &stop);
     if (rc) return rc;
-    sdk::check_kernel<<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n);
+    int variant = c->check_variant;
+    if (variant == SDK_CHECK_REG2 && tiles < 2ull * grid) variant = SDK_CHECK_REG1;   // rr2 needs a full tile per slot
+    switch (variant) {
+        case SDK_CHECK_REG2: sdk::check_kernel_rr2<<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
+        case SDK_CHECK_GLDS2: sdk::check_kernel_glds<2><<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
+        case SDK_CHECK_GLDS3: sdk::check_kernel_glds<3><<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
+        case SDK_CHECK_GLDS4: sdk::check_kernel_glds<4><<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
+        default: sdk::check_kernel<<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
+    }
     HIPCALL(hipGetLastError());
     HIPCALL(hipEventRecord(stop, c->stream));
     return SDK_OK;
@@ -422,6 +431,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 1 || value > 32) return fail(SDK_EINVAL, "waves per CU must be 1..32");
             c->waves_per_cu2 = (int)value;
             return SDK_OK;
+        case SDK_OPT_CHECK_VARIANT:
+            if (value < SDK_CHECK_REG1 || value > SDK_CHECK_GLDS4) return fail(SDK_EINVAL, "bad check variant %lld", (long long)value);
+            c->check_variant = (int)value;
+            return SDK_OK;
         default:
             return fail(SDK_EINVAL, "unknown option %d", key);
     }
@@ -439,6 +452,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_DEVICE_CUS: *value = c->cus; return SDK_OK;
         case SDK_OPT_SOLVER: *value = c->solver; return SDK_OK;
         case SDK_OPT_WAVES_PER_CU2: *value = c->waves_per_cu2; return SDK_OK;
+        case SDK_OPT_CHECK_VARIANT: *value = c->check_variant; return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }
 }

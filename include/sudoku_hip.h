@@ -70,6 +70,13 @@ extern "C" {
 #define SDK_OPT_DEVICE_CUS   6  /* read-only: compute units of the context's GPU        */
 #define SDK_OPT_SOLVER       7  /* solve kernel: SDK_SOLVER_* (default HALFWAVE)         */
 #define SDK_OPT_WAVES_PER_CU2 8 /* residency of the HALFWAVE solver, 1..32 (default 20) */
+#define SDK_OPT_CHECK_VARIANT 9 /* checker tile pipeline: SDK_CHECK_* (default REG1) */
+
+#define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
+#define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */
+#define SDK_CHECK_GLDS2      2  /* LDS-DMA ring of 2 tiles (check_kernel_glds<2>)      */
+#define SDK_CHECK_GLDS3      3  /* LDS-DMA ring of 3 tiles (check_kernel_glds<3>)      */
+#define SDK_CHECK_GLDS4      4  /* LDS-DMA ring of 4 tiles (check_kernel_glds<4>)      */
 
 #define SDK_SOLVER_WAVE      0  /* one board per wavefront (solve_kernel)              */
 #define SDK_SOLVER_HALFWAVE  1  /* two boards per wavefront, 27 lanes x 3 cells each   */

@@ -58,3 +58,35 @@ def test_one_million_synthetic(engine):
 
 def test_empty_batch(engine):
     assert engine.check_batch(np.zeros((0, 81), np.uint8)).shape == (0,)
+
+
+VARIANTS = [L.SDK_CHECK_REG1, L.SDK_CHECK_REG2, L.SDK_CHECK_GLDS2, L.SDK_CHECK_GLDS3, L.SDK_CHECK_GLDS4]
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_pipeline_variants_bit_exact(engine, variant):
+    """Every tile pipeline (register ring, LDS-DMA ring) gives the oracle's verdict bytes, at sizes that
+    hit every prologue/steady-state/tail combination of the grid (CUs x blocks/CU workgroups)."""
+    cus = engine.get_option(L.SDK_OPT_DEVICE_CUS)
+    rng = np.random.default_rng(11 + variant)
+    pool, pool_exp = synth.make_check_boards(1 << 18, seed=77)
+    odd = rng.integers(0, 20, (4096, 81)).astype(np.uint8)
+    odd_exp = O.check_batch(odd, threads=8)
+    try:
+        engine.set_option(L.SDK_OPT_CHECK_VARIANT, variant)
+        for bpc in (1, 2, 3, 4):
+            engine.set_option(L.SDK_OPT_CHECK_BLOCKS_PER_CU, bpc)
+            g = cus * bpc
+            for n in (1, 255, 256, 257, 256 * g - 1, 256 * g, 256 * g * 2 + 17, 256 * g * 3 + 256, 256 * g * 4 + 100):
+                idx = rng.integers(0, len(pool), n)
+                b, exp = pool[idx], pool_exp[idx]
+                if n > 8192:   # splice exact-path boards (values >= 10) into the middle and the tail
+                    b = b.copy(); exp = exp.copy()
+                    b[n // 2: n // 2 + 4096] = odd; exp[n // 2: n // 2 + 4096] = odd_exp
+                    b[-100:] = odd[:100]; exp[-100:] = odd_exp[:100]
+                v = engine.check_batch(b)
+                bad = np.flatnonzero(v != exp)
+                assert bad.size == 0, (variant, bpc, n, bad[:10])
+    finally:
+        engine.set_option(L.SDK_OPT_CHECK_VARIANT, L.SDK_CHECK_REG1)
+        engine.set_option(L.SDK_OPT_CHECK_BLOCKS_PER_CU, 3)

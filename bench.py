@@ -229,6 +229,39 @@ def c5_leg(eng, d, synth):
             "frontier_boards": size, "wall_ms": w * 1000.0, "value": total / w, "unit": "solutions/s"}
 
 
+C5_14CLUE_SOLUTIONS = 18_204_270   # the 15-clue board minus one more clue (C probe)
+
+
+def c5_rebalanced_leg(eng, d, synth):
+    """Config C5 on the 14-clue board with dynamic rebalancing: ranks start on equal blocks of the
+    replicated frontier and, after every round, all-gather their live ranges over RCCL (xGMI) so dry
+    ranks take half of the largest remaining one (shard.sharded_count_rebalanced)."""
+    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count_rebalanced
+    b15 = synth.SEEDS17["S1"][:-9] + "0" * 9
+    board = synth.parse(b15[:63] + "000100000" + "0" * 9)
+    comm = RcclComm(eng, d.rank, d.world) if d.world > 1 else None
+    try:
+        sharded_count_rebalanced(eng, board, d.rank, d.world, comm=comm)   # warm-up
+        walls = []
+        for _ in range(3):
+            info = {}
+            d.barrier()
+            t0 = time.perf_counter()
+            total, st, size = sharded_count_rebalanced(eng, board, d.rank, d.world, comm=comm, info=info)
+            walls.append(d.max(time.perf_counter() - t0))
+    finally:
+        if comm is not None:
+            comm.close()
+    w = min(walls)
+    return {"workload": "C5: count every completion of a 14-clue board (S1, last row cleared, one more clue "
+                        f"removed), rebalanced frontier over {d.world} GPU(s)"
+                        + (", RCCL all-gather of live ranges + all-reduce" if d.world > 1 else ""),
+            "solutions": total, "expected": C5_14CLUE_SOLUTIONS,
+            "ok": total == C5_14CLUE_SOLUTIONS and st == 1, "frontier_boards": size,
+            "rounds": info.get("rounds"), "steals": info.get("steals"),
+            "wall_ms": w * 1000.0, "value": total / w, "unit": "solutions/s"}
+
+
 def http_leg(requests):
     """Config C1: one puzzle POSTed to a single node's /solve (wiki 30-clue puzzle), end to end
     over loopback HTTP, on a GPU-backed node (distributed_sudoku_solver_amd.node)."""
@@ -422,6 +455,7 @@ def main():
     # ------------------------------------------------------------ C5 leg
     if args.count_leg:
         result["c5_count"] = c5_leg(eng, d, synth)
+        result["c5_count_rebalanced"] = c5_rebalanced_leg(eng, d, synth)
 
     # ---------------------------------------------------------- CPU baseline
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:

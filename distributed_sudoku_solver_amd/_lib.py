@@ -87,6 +87,7 @@ SIGNATURES = {
     "sdk_comm_destroy": (ctypes.c_int, [_vp]),
     "sdk_comm_allreduce_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int, ctypes.c_int]),
     "sdk_comm_broadcast_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int]),
+    "sdk_comm_allgather_dev": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
     "sdk_dev_alloc": (ctypes.c_int, [_vp, _sz, ctypes.POINTER(_vp)]),
     "sdk_dev_free": (ctypes.c_int, [_vp, _vp]),
     "sdk_memcpy_h2d": (ctypes.c_int, [_vp, _vp, _vp, _sz]),

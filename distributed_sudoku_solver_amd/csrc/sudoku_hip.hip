@@ -689,4 +689,13 @@ int sdk_comm_broadcast_dev(sdk_ctx* c, void* d_buf, size_t bytes, int root) {
     return SDK_OK;
 }
 
+int sdk_comm_allgather_dev(sdk_ctx* c, const void* d_send, void* d_recv, size_t bytes) {
+    if (!c || (bytes && (!d_send || !d_recv))) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->comm) return fail(SDK_EINVAL, "no communicator: call sdk_comm_init first");
+    HIPCALL(hipSetDevice(c->device));
+    NCCLCALL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, c->comm, c->stream));
+    return SDK_OK;
+}
+
 }  // extern "C"

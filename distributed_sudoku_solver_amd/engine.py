@@ -261,6 +261,10 @@ class SudokuEngine:
     def comm_broadcast(self, d_buf, nbytes, root):
         L.check(self.lib.sdk_comm_broadcast_dev(self.ctx, d_buf.ptr, int(nbytes), int(root)), "sdk_comm_broadcast_dev")
 
+    def comm_allgather(self, d_send, d_recv, nbytes):
+        L.check(self.lib.sdk_comm_allgather_dev(self.ctx, d_send.ptr, d_recv.ptr, int(nbytes)),
+                "sdk_comm_allgather_dev")
+
     # --------------------------------------------------------- device batch
     def check_batch_dev(self, d_boards, d_verdict, n):
         L.check(self.lib.sdk_check_batch_dev(self.ctx, d_boards.ptr, d_verdict.ptr, int(n)), "sdk_check_batch_dev")

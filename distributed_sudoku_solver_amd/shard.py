@@ -187,6 +187,9 @@ class RcclComm:
     def broadcast(self, buf, nbytes, root):
         self.engine.comm_broadcast(buf, nbytes, root)
 
+    def allgather(self, send, recv, nbytes):
+        self.engine.comm_allgather(send, recv, nbytes)
+
     def close(self):
         self.engine.comm_destroy()
 
@@ -213,6 +216,14 @@ class HostComm:
         t = torch.from_numpy(buf.view(np.uint8)[:nbytes].copy())
         dist.broadcast(t, src=root, group=self.group)
         buf.view(np.uint8)[:nbytes] = t.numpy()
+
+    def allgather(self, send, recv, nbytes):
+        import torch
+        import torch.distributed as dist
+        t = torch.from_numpy(send.view(np.uint8)[:nbytes].copy())
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t, group=self.group)
+        recv.view(np.uint8)[:self.world * nbytes] = torch.cat(parts).numpy()
 
     def close(self):
         pass
@@ -283,3 +294,99 @@ def sharded_solve(engine, board, rank, world, comm=None, mask=None, waves=8, tar
             if hasattr(h, "free"):
                 h.free()
     return board.copy(), 0
+
+
+def _store(buf, values, dtype):
+    arr = np.asarray(values, dtype=dtype)
+    if hasattr(buf, "upload"):
+        buf.upload(arr)
+    else:
+        buf[:len(arr)] = arr
+
+
+def rebalance_ranges(ranges, min_split=2):
+    """One rebalancing step over the all-gathered live ranges [lo, hi) of the ranks.
+
+    In rank order, every rank whose range is empty takes the upper half of the currently largest
+    remaining range (ties -> lowest rank); ranges shorter than `min_split` are not split.  A pure
+    function of the gathered values, so every rank computes the same assignment and only the
+    2 x int64 per rank travel (the frontier itself is replicated)."""
+    R = [[int(a), int(b)] for a, b in ranges]
+    for r in range(len(R)):
+        if R[r][1] > R[r][0]:
+            continue
+        donor = max(range(len(R)), key=lambda k: (R[k][1] - R[k][0], -k))
+        rem = R[donor][1] - R[donor][0]
+        if rem < max(2, min_split):
+            continue
+        mid = R[donor][0] + rem // 2
+        R[r] = [mid, R[donor][1]]
+        R[donor][1] = mid
+    return R
+
+
+def sharded_count_rebalanced(engine, board, rank, world, limit=0, comm=None, target=None, chunk=None, info=None,
+                             ranges=None):
+    """sharded_count with dynamic rebalancing of the replicated frontier.
+
+    Each rank starts on a contiguous block of the frontier and counts it `chunk` boards per round.
+    After every round the ranks all-gather their live ranges (RCCL ncclAllGather of 2 x int64 per
+    rank on device memory, or gloo in the CPU tests) and ranks that ran dry take the upper half of
+    the largest remaining range (rebalance_ranges).  Subtree sizes are heavy-tailed, so a static split
+    leaves GPUs idle behind the rank holding the heavy boards; here they finish within about one
+    round of each other.  Counts are combined by one all-reduce(sum) at the end.
+    `ranges` (optional, one (lo, hi) per rank, same on every rank) replaces the initial equal blocks,
+    e.g. to resume a partial count.
+    Returns (total, status, frontier_size) like sharded_count; `info` (dict) gets rounds/steals."""
+    if world > 1 and comm is None:
+        raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
+    size, leaves = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT,
+                                         target=default_target(engine, world) if target is None else target)
+    if chunk is None:
+        chunk = max(1, default_target(engine, 1) // 4)        # 2 boards per resident solver wave
+    lo, hi = shard_bounds(size, rank, world) if ranges is None else (int(ranges[rank][0]), int(ranges[rank][1]))
+    lo, hi = min(lo, size), min(hi, size)
+    res = engine.result_buffer(2, np.uint64)
+    mine = engine.result_buffer(2, np.int64)
+    allr = engine.result_buffer(2 * world, np.int64)
+    tot = engine.result_buffer(2, np.uint64)
+    count = hits = rounds = steals = 0
+    try:
+        while True:
+            end = min(hi, lo + chunk)
+            if end > lo:
+                engine.frontier_count(lo, 1, end, limit, res)
+                c, h = (int(x) for x in engine.read(res, 2, np.uint64))
+                count += c
+                hits += h
+                lo = end
+                if limit and count >= limit:
+                    lo = hi                                    # this rank alone reached the limit
+            rounds += 1
+            if comm is None:                                   # single rank, nothing to exchange
+                if lo >= hi:
+                    break
+                continue
+            _store(mine, [lo, hi], np.int64)
+            comm.allgather(mine, allr, 16)
+            R = engine.read(allr, 2 * world, np.int64).reshape(world, 2)
+            if all(b <= a for a, b in R):
+                break
+            newR = rebalance_ranges(R, min_split=max(2, chunk // 2))
+            steals += sum(1 for a, b in zip(R.tolist(), newR) if a != b and a[1] <= a[0])
+            lo, hi = newR[rank]
+        _store(tot, [count, hits], np.uint64)
+        if comm is not None:
+            comm.allreduce(tot, 2, np.uint64, "sum")
+        count, hits = (int(x) for x in engine.read(tot, 2, np.uint64))
+    finally:
+        for h in (res, mine, allr, tot):
+            if hasattr(h, "free"):
+                h.free()
+    if info is not None:
+        info.update(rounds=rounds, steals=steals, chunk=chunk)
+    total = count + leaves
+    if limit and total > limit:
+        total = limit
+    st = -2 if hits else (1 if total > 0 else 0)
+    return total, st, size

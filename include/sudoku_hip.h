@@ -179,6 +179,9 @@ int sdk_comm_destroy(sdk_ctx *ctx);
 /* In place, on device memory, enqueued on the context stream. */
 int sdk_comm_allreduce_dev(sdk_ctx *ctx, void *d_buf, size_t count, int dtype, int op);
 int sdk_comm_broadcast_dev(sdk_ctx *ctx, void *d_buf, size_t bytes, int root);
+/* d_recv[r*bytes .. (r+1)*bytes) = rank r's d_send (ncclAllGather): the live-range
+ * exchange of the rebalanced frontier count (shard.sharded_count_rebalanced). */
+int sdk_comm_allgather_dev(sdk_ctx *ctx, const void *d_send, void *d_recv, size_t bytes);
 
 /* ---- device-pointer API (asynchronous on the context stream) ------------ */
 int sdk_dev_alloc(sdk_ctx *ctx, size_t bytes, void **dptr);

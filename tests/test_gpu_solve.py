@@ -270,7 +270,7 @@ def test_rccl_communicator_world1(engine):
     """RCCL path end to end on one GPU: communicator of size 1, device all-reduce /
     broadcast inside sharded_count and sharded_solve."""
     from distributed_sudoku_solver_amd.engine import SudokuEngine
-    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count, sharded_solve
+    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count, sharded_count_rebalanced, sharded_solve
     eng = SudokuEngine(0)
     try:
         comm = RcclComm(eng, 0, 1, uid=SudokuEngine.comm_unique_id())
@@ -284,6 +284,17 @@ def test_rccl_communicator_world1(engine):
         out, st = sharded_solve(eng, synth.parse(DEMO), 0, 1, comm=comm)
         assert st == 1 and "".join(map(str, out)) == \
             "234156789179328456568479132391245678425687391687913245752831964816794523943562817"
+        # all-gather (the rebalancing exchange) and the rebalanced count through it
+        src = eng.result_buffer(2, np.int64)
+        dst = eng.result_buffer(2, np.int64)
+        src.upload(np.array([11, -3], np.int64))
+        comm.allgather(src, dst, 16)
+        assert eng.read(dst, 2, np.int64).tolist() == [11, -3]
+        src.free(); dst.free()
+        info = {}
+        assert sharded_count_rebalanced(eng, synth.parse(s1[:-9] + "0" * 9), 0, 1, comm=comm, chunk=4096,
+                                        info=info)[:2] == (3481026, 1)
+        assert info["rounds"] > 3
         comm.close()
     finally:
         eng.close()

@@ -8,8 +8,8 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from distributed_sudoku_solver_amd.shard import (HostComm, MultiDeviceEngine, ShardedBatch, shard_bounds,
-                                                 sharded_count, sharded_solve)
+from distributed_sudoku_solver_amd.shard import (HostComm, MultiDeviceEngine, ShardedBatch, rebalance_ranges,
+                                                 shard_bounds, sharded_count, sharded_count_rebalanced, sharded_solve)
 from distributed_sudoku_solver_amd import synth, _lib as L
 
 
@@ -128,6 +128,14 @@ def _worker(rank, world, port, q):
         if rank == 0:
             q.put(("count", total == 7309 and st == 1 and size >= 32))
         q.put(("count_split", rank, counted, size))
+        # rebalanced count: rank 0 starts with the whole frontier, rank 1 must steal over gloo
+        eng.calls = []
+        info = {}
+        b16 = synth.parse(s1[:-9] + "000800000")
+        total, st, size = sharded_count_rebalanced(eng, b16, rank, world, comm=comm, chunk=2, info=info,
+                                                   ranges=[(0, 10 ** 9), (0, 0)])
+        idx = sorted(i for c in eng.calls if c[0] == "count" for i in c[1])
+        q.put(("rebal", rank, total == 7309 and st == 1, idx, size, info["steals"]))
         # first solution of the multi-solution demo board (sudoku.py:99-109) = reference golden
         demo = synth.parse("000100000000320000000009000000000070000000000000900000000000900000000003000000000")
         golden = "234156789179328456568479132391245678425687391687913245752831964816794523943562817"
@@ -167,8 +175,14 @@ def test_world2_gloo_gather():
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    got = [q.get(timeout=5) for _ in range(3 + 5 * world)]
-    res = {g[0]: g[1:] for g in got if g[0] not in ("calls", "count_split", "first", "first_range", "unsolvable")}
+    got = [q.get(timeout=5) for _ in range(3 + 6 * world)]
+    res = {g[0]: g[1:] for g in got if g[0] not in ("calls", "count_split", "first", "first_range", "unsolvable",
+                                                    "rebal")}
+    rebal = {g[1]: g[2:] for g in got if g[0] == "rebal"}
+    assert rebal[0][0] and rebal[1][0]                                      # same total on both ranks
+    fsize = rebal[0][2]
+    assert sorted(rebal[0][1] + rebal[1][1]) == list(range(fsize))         # disjoint and complete
+    assert len(rebal[1][1]) > 0 and rebal[1][3] >= 1                        # rank 1 stole work
     assert res["solve"] == (True,) and res["check"] == (True,) and res["count"] == (True,)
     for key in ("first", "first_range", "unsolvable"):
         assert sorted(g[1:] for g in got if g[0] == key) == [(r, True) for r in range(world)], key
@@ -188,3 +202,23 @@ def test_multi_device_engine_threads():
     b, exp = synth.make_check_boards(1000, seed=9)
     assert (mde.check_batch(b) == exp).all()
     assert [e.calls for e in engines] == [[33, 333], [33, 333], [34, 334]]
+
+
+def test_rebalance_ranges():
+    # dry ranks take the upper half of the largest live range, in rank order; ties -> lowest rank
+    assert rebalance_ranges([[5, 5], [0, 100], [10, 20]]) == [[50, 100], [0, 50], [10, 20]]
+    assert rebalance_ranges([[0, 0], [0, 0], [0, 64]]) == [[32, 48], [48, 64], [0, 32]]
+    assert rebalance_ranges([[0, 8], [0, 8], [3, 3]]) == [[0, 4], [0, 8], [4, 8]]
+    assert rebalance_ranges([[0, 3], [7, 7]], min_split=4) == [[0, 3], [7, 7]]   # too short to split
+    assert rebalance_ranges([[1, 1], [2, 2]]) == [[1, 1], [2, 2]]                 # all done
+    rng = np.random.default_rng(0)
+    for _ in range(200):                           # conservation: the live work is only re-partitioned
+        w = int(rng.integers(1, 9))
+        R = []
+        for _ in range(w):
+            lo = int(rng.integers(0, 1000))
+            R.append([lo, lo + int(rng.integers(0, 50)) * int(rng.integers(0, 2))])
+        N = rebalance_ranges(R)
+        before = sorted(i for a, b in R for i in range(a, b))
+        after = sorted(i for a, b in N for i in range(a, b))
+        assert before == after

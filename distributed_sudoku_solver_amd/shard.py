@@ -342,8 +342,8 @@ def sharded_count_rebalanced(engine, board, rank, world, limit=0, comm=None, tar
         raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
     size, leaves = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT,
                                          target=default_target(engine, world) if target is None else target)
-    if chunk is None:
-        chunk = max(1, default_target(engine, 1) // 4)        # 2 boards per resident solver wave
+    if chunk is None:   # one launch when there is no one to rebalance with; else 2 boards per resident wave
+        chunk = max(1, size) if comm is None else max(1, default_target(engine, 1) // 4)
     lo, hi = shard_bounds(size, rank, world) if ranges is None else (int(ranges[rank][0]), int(ranges[rank][1]))
     lo, hi = min(lo, size), min(hi, size)
     res = engine.result_buffer(2, np.uint64)

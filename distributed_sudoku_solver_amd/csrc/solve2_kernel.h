@@ -82,10 +82,12 @@ __device__ __forceinline__ void init_lane2(Lane2& w, uint32_t* s_cell_all, uint3
     } else {
         // lanes 27..31 run the same instructions on spare slots (cells 81..95, units
         // 27..31) with inert cells, so the round needs no exec-mask branches
+        // (slot banks chosen so no write shares a bank with a real cell of the same
+        // store: c0 stores hit banks 0..26, c1 27..31+0..21, c2 22..31+0..16)
         const int e = w.hl - 27;
-        w.c0 = 81 + e;
+        w.c0 = 91 + e;
         w.c1 = 86 + e;
-        w.c2 = 91 + e;
+        w.c2 = 81 + e;
         w.ucol = w.ur0 = w.ur1 = w.ur2 = w.ub0 = w.ub1 = w.ub2 = 27 + e;
     }
     // unit j's cell holding digit k+1 of G (see the header); spare lanes copy lane 0

@@ -47,7 +47,7 @@
 
 namespace sdk {
 
-constexpr int kLdsLevels = 12;                     // 12 x 512 B per wave in LDS
+constexpr int kLdsLevels = 10;                     // 10 x 512 B per wave in LDS (24 waves/CU fit)
 constexpr int kStack2WordsPerBlock = kMaxDepth * 64 * 2;
 
 struct Lane2 {
@@ -324,7 +324,7 @@ __device__ __forceinline__ void finish_board(const Lane2& w, const Args2& a, Boa
 }
 
 #ifdef SDK_DEFINE_SOLVE2_KERNEL   // defined in solve2_launch.hip only
-__global__ __launch_bounds__(64) void solve2_kernel(SolveArgs args) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void solve2_kernel(SolveArgs args) {
     __shared__ uint32_t s_cell[2 * 96];
     __shared__ uint32_t s_unit[2 * 32];
     __shared__ uint32_t s_br[2][kMaxDepth];

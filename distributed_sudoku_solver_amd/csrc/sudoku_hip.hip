@@ -67,7 +67,8 @@ struct sdk_ctx {
     int check_variant = SDK_CHECK_REG1;
     int work_rounds = 0;
     int solver = SDK_SOLVER_HALFWAVE;
-    int waves_per_cu2 = 20;       // residency of solve2_kernel (LDS caps it at 20 per CU)
+    int waves_per_cu2 = 32;       // solve2_kernel grid per CU (24 resident: 80 VGPRs, 6.8 KB LDS; the rest
+                                  // start as the first retire, and the smaller dequeue chunk trims the tail)
     // workspaces
     DevBuf stack, counter, in, mask, out, status, work, verdict;
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask;

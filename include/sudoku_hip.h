@@ -69,7 +69,7 @@ extern "C" {
 #define SDK_OPT_WORK_COUNTER 5  /* what solve `work` counts: SDK_WORK_* (default nodes) */
 #define SDK_OPT_DEVICE_CUS   6  /* read-only: compute units of the context's GPU        */
 #define SDK_OPT_SOLVER       7  /* solve kernel: SDK_SOLVER_* (default HALFWAVE)         */
-#define SDK_OPT_WAVES_PER_CU2 8 /* residency of the HALFWAVE solver, 1..32 (default 20) */
+#define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE solver per CU, 1..32 (default 32) */
 #define SDK_OPT_CHECK_VARIANT 9 /* checker tile pipeline: SDK_CHECK_* (default REG1) */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */

@@ -143,9 +143,14 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     const bool two = !count_mode && c->solver == SDK_SOLVER_HALFWAVE;
     if (two && (!d_out || !d_status)) return fail(SDK_EINVAL, "solve needs out and status buffers");
     const uint64_t slots = (uint64_t)c->cus * (two ? c->waves_per_cu2 : c->waves_per_cu) * (two ? 2 : 1);
-    // ~16 dequeues per board slot over the launch, 1..64 boards each; count mode
-    // uses single boards (subtrees differ by orders of magnitude)
-    const uint32_t chunk = count_mode ? 1u : (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, n / (slots * 16)));
+    // ~16 dequeues per board slot over the launch, 1..64 boards each, but at least 16
+    // boards (while every slot still gets >= 2 dequeues): all dequeues hit ONE counter,
+    // whose same-address atomics serialise at ~10 ns each, so cheap boards (C2: 1M
+    // propagation-only puzzles) would otherwise be dequeue-bound.  Count mode uses
+    // single boards (subtrees differ by orders of magnitude).
+    const uint64_t floor16 = std::min<uint64_t>(16, std::max<uint64_t>(1, n / (slots * 2)));
+    const uint32_t chunk = count_mode ? 1u
+        : (uint32_t)std::max<uint64_t>(floor16, std::min<uint64_t>(64, std::max<uint64_t>(1, n / (slots * 16))));
     const uint64_t want = (n + chunk - 1) / chunk;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(two ? (want + 1) / 2 : want,
                                                                              two ? slots / 2 : slots));

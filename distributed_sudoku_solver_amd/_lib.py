@@ -33,6 +33,7 @@ SDK_OPT_DEVICE_CUS = 6
 SDK_OPT_SOLVER = 7
 SDK_OPT_WAVES_PER_CU2 = 8
 SDK_OPT_CHECK_VARIANT = 9
+SDK_OPT_SOLVE_CHUNK = 10
 SDK_CHECK_REG1 = 0
 SDK_CHECK_REG2 = 1
 SDK_CHECK_GLDS2 = 2

@@ -65,6 +65,7 @@ struct sdk_ctx {
     int waves_per_cu = 32;
     int check_blocks_per_cu = 3;
     int check_variant = SDK_CHECK_REG1;
+    int solve_chunk = 0;          // boards per dequeue, 0 = automatic
     int work_rounds = 0;
     int solver = SDK_SOLVER_HALFWAVE;
     int waves_per_cu2 = 32;       // solve2_kernel grid per CU (24 resident: 80 VGPRs, 6.8 KB LDS; the rest
@@ -143,14 +144,14 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     const bool two = !count_mode && c->solver == SDK_SOLVER_HALFWAVE;
     if (two && (!d_out || !d_status)) return fail(SDK_EINVAL, "solve needs out and status buffers");
     const uint64_t slots = (uint64_t)c->cus * (two ? c->waves_per_cu2 : c->waves_per_cu) * (two ? 2 : 1);
-    // ~16 dequeues per board slot over the launch, 1..64 boards each, but at least 16
-    // boards (while every slot still gets >= 2 dequeues): all dequeues hit ONE counter,
-    // whose same-address atomics serialise at ~10 ns each, so cheap boards (C2: 1M
-    // propagation-only puzzles) would otherwise be dequeue-bound.  Count mode uses
-    // single boards (subtrees differ by orders of magnitude).
-    const uint64_t floor16 = std::min<uint64_t>(16, std::max<uint64_t>(1, n / (slots * 2)));
+    // 16 boards per dequeue (fewer when a slot would get < 2 dequeues).  All dequeues hit ONE
+    // counter and same-address atomics serialise at ~10 ns each: below ~16 boards the cheap
+    // C2 boards (1.15 ns per board chip-wide) become dequeue-bound; above it the C4 tail grows
+    // (tools/sweep_chunk.py: chunk 8/16/32/64 = 411/409/404/393M 17-clue puzzles/s).
+    // Count mode uses single boards (subtrees differ by orders of magnitude).
     const uint32_t chunk = count_mode ? 1u
-        : (uint32_t)std::max<uint64_t>(floor16, std::min<uint64_t>(64, std::max<uint64_t>(1, n / (slots * 16))));
+        : c->solve_chunk ? (uint32_t)c->solve_chunk
+        : (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, n / (slots * 2)));
     const uint64_t want = (n + chunk - 1) / chunk;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(two ? (want + 1) / 2 : want,
                                                                              two ? slots / 2 : slots));
@@ -437,6 +438,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 1 || value > 32) return fail(SDK_EINVAL, "waves per CU must be 1..32");
             c->waves_per_cu2 = (int)value;
             return SDK_OK;
+        case SDK_OPT_SOLVE_CHUNK:
+            if (value < 0 || value > 4096) return fail(SDK_EINVAL, "solve chunk must be 0..4096");
+            c->solve_chunk = (int)value;
+            return SDK_OK;
         case SDK_OPT_CHECK_VARIANT:
             if (value < SDK_CHECK_REG1 || value > SDK_CHECK_GLDS4) return fail(SDK_EINVAL, "bad check variant %lld", (long long)value);
             c->check_variant = (int)value;
@@ -459,6 +464,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_SOLVER: *value = c->solver; return SDK_OK;
         case SDK_OPT_WAVES_PER_CU2: *value = c->waves_per_cu2; return SDK_OK;
         case SDK_OPT_CHECK_VARIANT: *value = c->check_variant; return SDK_OK;
+        case SDK_OPT_SOLVE_CHUNK: *value = c->solve_chunk; return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }
 }

@@ -71,6 +71,7 @@ extern "C" {
 #define SDK_OPT_SOLVER       7  /* solve kernel: SDK_SOLVER_* (default HALFWAVE)         */
 #define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE solver per CU, 1..32 (default 32) */
 #define SDK_OPT_CHECK_VARIANT 9 /* checker tile pipeline: SDK_CHECK_* (default REG1) */
+#define SDK_OPT_SOLVE_CHUNK  10  /* boards per solver dequeue, 0 = automatic (default)  */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

@@ -325,3 +325,16 @@ def test_solvers_take_identical_search_paths(engine):
         a, b = res[(SOLVERS[0], kind)], res[(SOLVERS[1], kind)]
         assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
         assert (a[2] == b[2]).all(), kind
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 100, 4096])
+def test_dequeue_chunk_override(engine, chunk):
+    """Any boards-per-dequeue gives the same boards (chunks straddling the batch end included)."""
+    p, s = synth.make_17clue(20_011, seed=77)
+    try:
+        engine.set_option(L.SDK_OPT_SOLVE_CHUNK, chunk)
+        for n in (1, 33, 20_011):
+            out, st, _ = engine.solve_batch(p[:n])
+            assert (st == 1).all() and (out == s[:n]).all(), (chunk, n)
+    finally:
+        engine.set_option(L.SDK_OPT_SOLVE_CHUNK, 0)

@@ -2,12 +2,18 @@
 """Benchmark of the hot path on MI355X (contract: one JSON line from rank 0).
 
 Headline (BASELINE.json metric): 17-clue hard puzzles solved per second, whole
-job, config C4 = 10M transformed 17-clue puzzles per GPU resident in HBM; one
-"step" = one sdk_solve_batch_dev pass over the batch.  Ranks shard the puzzle
-stream with no collective on the data path (weak scaling: each GPU owns its own
-batch); torch.distributed (gloo) is used only for the barrier and the max-over-
-ranks time.  After timing, every solved board is compared with its expected
-solution (known by construction) -- a mismatch fails the run.
+job, config C4 = 10M transformed 17-clue puzzles SHARDED over the N GPUs (rank k
+owns rows [k*10M/N, (k+1)*10M/N) of one seeded stream, resident in HBM; strong
+scaling); one "step" = one sdk_solve_batch_dev pass of every rank over its
+slice.  No collective on the data path; torch.distributed (gloo) carries only
+the barrier and the max-over-ranks time.  After timing, every solved board is
+compared with its expected solution (known by construction) -- a mismatch fails
+the run.  At N > 1 a secondary weak-scaling figure (10M puzzles per GPU) is
+reported beside it.
+
+`python bench.py --gpus N` without torchrun starts N rank processes itself (one
+per GPU, before anything touches a GPU); under torchrun the ranks come from
+RANK / WORLD_SIZE / LOCAL_RANK.
 
 Side legs on the same run: the batched checker (config C3, 100M boards per GPU
 by default, HBM-bound), config C2 (1M ~30-clue puzzles per GPU), config C5 (an
@@ -31,6 +37,14 @@ METRIC = "puzzles solved/sec (whole node, 17-clue hard) at 1/2/4/8 GPUs; checker
 HBM_PEAK_GBPS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 SOLVE_BYTES_PER_PUZZLE = 163      # 81 in + 81 out + 1 status
 CHECK_BYTES_PER_BOARD = 82        # 81 in + 1 verdict
+# VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles (32 lanes/cycle x 2)")
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
+# --solver: (SDK_OPT_SOLVER value, kernel name, grid option) -- resolved after the library loads
+SOLVERS = {
+    "halfwave": (1, "sdk::solve2_kernel", 8),
+    "wave": (0, "sdk::solve_kernel", 3),
+}
 
 
 def parse_args():
@@ -39,17 +53,22 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=["solve17", "solve30"], default="solve17")
-    ap.add_argument("--batch", type=int, default=10_000_000, help="puzzles per GPU")
+    ap.add_argument("--batch", type=int, default=10_000_000, help="C4 puzzles, whole job (sharded over the GPUs)")
+    ap.add_argument("--weak-leg", type=int, default=1, help="N > 1: also time --batch puzzles per GPU (weak scaling)")
     ap.add_argument("--check-boards", type=int, default=100_000_000, help="checker boards per GPU (0 = skip)")
     ap.add_argument("--check-steps", type=int, default=10)
     ap.add_argument("--check-warmup", type=int, default=10,
                     help="untimed checker launches first (the memory clocks ramp under sustained streaming)")
     ap.add_argument("--order", choices=["mrv_unique", "lex"], default="mrv_unique")
-    ap.add_argument("--solver", choices=["halfwave", "wave"], default="halfwave",
+    ap.add_argument("--solver", choices=sorted(SOLVERS), default="halfwave",
                     help="solve kernel: two boards per wave (solve2_kernel) or one (solve_kernel)")
     ap.add_argument("--waves-per-cu", type=int, default=None)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget per leg (0 = skip)")
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="CPU baseline processes/threads (0 = this process's CPU share: affinity, capped by "
+                         "OMP_NUM_THREADS when set)")
+    ap.add_argument("--cpu-puzzle-budget", type=int, default=2_000_000,
+                    help="per-puzzle timeout of the Python baseline, in reference validations")
     ap.add_argument("--http-requests", type=int, default=20, help="C1 POST /solve leg (rank 0, N=1; 0 = skip)")
     ap.add_argument("--seed", type=int, default=20250614)
     ap.add_argument("--c2-puzzles", type=int, default=1_000_000,
@@ -57,9 +76,10 @@ def parse_args():
     ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
                     help="watchdog for the side legs: print what was measured and exit")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
-                    help="per-launch HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this bench "
-                         "(tools/gpu_round.sh pmc); '' = report traffic null")
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02", "pmc_c4.json"),
+                    help="per-launch PMC figures of the C4 solve kernel and the C3 checker from rocprofv3 passes "
+                         "of this bench at its default sizes (tools/pmc_c4.sh); '' = report traffic null")
+    ap.add_argument("--engine-factory", default="", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -100,17 +120,30 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def pmc_traffic(path, kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_summary.py:
-    2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
+def pmc_record(path, kernel, units):
+    """Per-launch PMC figures of `kernel` from the committed rocprofv3 passes of this bench
+    (tools/pmc_c4.sh -> tools/pmc_summary.py), or None.  Only used when the record was taken at
+    the same units per launch as this run (puzzles or boards per launch)."""
     if not path or not os.path.exists(path):
         return None
     with open(path) as f:
         rec = json.load(f).get(kernel)
-    return None if rec is None else float(rec["traffic_bytes"])
+    if rec is None or int(rec.get("units_per_launch", -1)) != int(units):
+        return None
+    return rec
 
 
-def cpu_baseline(puzzles, seconds, threads):
+def cpu_share():
+    """CPU cores this process may use: its affinity set, capped by OMP_NUM_THREADS when set
+    (the GPU box exports its per-GPU CPU share there; os.cpu_count() is the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline_c(puzzles, seconds, threads):
     """Oracle's C port of the reference naive DFS (DHT_Node.py:474-538), timed on this
     host on a bounded prefix of the SAME puzzle batch, `threads` puzzles at a time."""
     from oracle import oracle as O
@@ -129,44 +162,47 @@ def cpu_baseline(puzzles, seconds, threads):
         "unit": "puzzles/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"first {done} puzzles of the rank-0 batch, naive DFS (oracle/sudoku_oracle.c, "
+        "sample": (f"first {done} puzzles of the rank-0 batch, naive DFS in C (oracle/sudoku_oracle.c, "
                    f"restates DHT_Node.py:474-538, validations-exact), {threads} threads, "
                    f"{wall:.1f} s wall, {timeouts} hit the 2e9-validation budget"),
     }
 
 
-def cpu_baseline_python(puzzles, seconds, procs):
+def cpu_baseline_python(puzzles, seconds, procs, budget, what):
     """The oracle's line-by-line Python restatement of DHTNode.solve_sudoku
     (oracle.py_naive_solve, DHT_Node.py:474-538) -- the closest stand-in for the
     reference's own Python solver, which cannot travel to the GPU box -- one process
-    per core (like one DHT node per core), each on its own slice of the batch."""
+    per core (like one DHT node per core, -d 0), each on its own slice of the batch,
+    every puzzle capped at `budget` validations (the per-puzzle timeout)."""
     import multiprocessing as mp
     from oracle import oracle as O
-    per = max(1, int(seconds / 0.01))          # more than a process can finish
+    per = max(1, -(-len(puzzles) // procs))
     slices = [[list(map(int, puzzles[i])) for i in range(k * per, min((k + 1) * per, len(puzzles)))]
               for k in range(procs)]
     t0 = time.perf_counter()
     with mp.get_context("spawn").Pool(procs) as pool:
-        res = pool.starmap(O.py_solve_timed, [(sl, seconds) for sl in slices])
+        res = pool.starmap(O.py_solve_timed, [(sl, seconds, budget) for sl in slices])
     wall = time.perf_counter() - t0
     done = sum(r[0] for r in res)
     solved = sum(r[1] for r in res)
     busy = max(r[2] for r in res)
+    timeouts = sum(r[3] for r in res)
     return {
         "value": solved / busy if busy > 0 else 0.0,
         "unit": "puzzles/s",
         "cores": procs,
         "kind": "port",
-        "sample": (f"{done} puzzles of the rank-0 batch ({procs} disjoint slices), pure-Python naive DFS "
-                   f"(oracle/oracle.py py_naive_solve, restates DHT_Node.py:474-538 line by line), "
-                   f"{procs} processes, {busy:.1f} s solving ({wall:.1f} s incl. process start)"),
+        "sample": (f"{what}: {done} puzzles attempted in {procs} disjoint slices, one process per core, "
+                   f"pure-Python naive DFS (oracle/oracle.py py_naive_solve, restates DHT_Node.py:474-538 "
+                   f"line by line, -d 0), {solved} solved, {timeouts} stopped at the {budget:,}-validation "
+                   f"per-puzzle timeout, {busy:.1f} s solving per process ({wall:.1f} s incl. process start)"),
     }
 
 
 def c2_leg(eng, d, args, synth):
     """Config C2: ~30-clue unique puzzles, resident in HBM, one launch per step."""
     n = args.c2_puzzles
-    p, sol = synth.make_30clue(n, seed=args.seed + 31 + 1000 * d.rank)
+    p, sol = synth.make_30clue(n, seed=args.seed + 31, lo=d.rank * n)
     d_in, d_out, d_st = eng.alloc(n * 81), eng.alloc(n * 81), eng.alloc(n)
     d_in.upload(p)
     eng.solve_batch_dev(d_in, d_out, d_st, n)
@@ -196,9 +232,10 @@ def c2_leg(eng, d, args, synth):
                         "kernel": args.solve_kernel},
            "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
-        cores = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        leg["cpu_baseline"] = cpu_baseline(p, min(5.0, args.cpu_seconds), cores)
-        leg["cpu_baseline_python"] = cpu_baseline_python(p, min(5.0, args.cpu_seconds), cores)
+        cores = args.cpu_cores or cpu_share()
+        leg["cpu_baseline"] = cpu_baseline_python(p[:200_000], min(5.0, args.cpu_seconds), cores,
+                                                  args.cpu_puzzle_budget, "C2 ~30-clue sample")
+        leg["cpu_baseline_c_port"] = cpu_baseline_c(p, min(5.0, args.cpu_seconds), cores)
     return leg
 
 
@@ -208,9 +245,9 @@ C5_BOARD_SOLUTIONS = 3_481_026    # S1 with its last row clear
 def c5_leg(eng, d, synth):
     """Config C5: exhaustive count of one 15-clue board.  Every rank expands the same frontier
     and counts its interleaved share; one RCCL all-reduce (device memory, xGMI) combines them."""
-    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count
+    from distributed_sudoku_solver_amd.shard import HostComm, RcclComm, sharded_count
     board = synth.parse(synth.SEEDS17["S1"][:-9] + "0" * 9)
-    comm = RcclComm(eng, d.rank, d.world) if d.world > 1 else None
+    comm = RcclComm(eng, d.rank, d.world, transport=HostComm(d.rank, d.world)) if d.world > 1 else None
     try:
         sharded_count(eng, board, d.rank, d.world, comm=comm)            # warm-up
         walls = []
@@ -236,10 +273,10 @@ def c5_rebalanced_leg(eng, d, synth):
     """Config C5 on the 14-clue board with dynamic rebalancing: ranks start on equal blocks of the
     replicated frontier and, after every round, all-gather their live ranges over RCCL (xGMI) so dry
     ranks take half of the largest remaining one (shard.sharded_count_rebalanced)."""
-    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count_rebalanced
+    from distributed_sudoku_solver_amd.shard import HostComm, RcclComm, sharded_count_rebalanced
     b15 = synth.SEEDS17["S1"][:-9] + "0" * 9
     board = synth.parse(b15[:63] + "000100000" + "0" * 9)
-    comm = RcclComm(eng, d.rank, d.world) if d.world > 1 else None
+    comm = RcclComm(eng, d.rank, d.world, transport=HostComm(d.rank, d.world)) if d.world > 1 else None
     try:
         sharded_count_rebalanced(eng, board, d.rank, d.world, comm=comm)   # warm-up
         walls = []
@@ -292,18 +329,80 @@ def http_leg(requests):
             "reference_note": "DHT_Node.py single node, -d 0, measured in the build container (SURVEY §3.1)"}
 
 
+def launch_ranks(args):
+    """`--gpus N` without torchrun: start N rank processes of this script (one per GPU) with
+    the torchrun environment, before this process touches any GPU; rank 0 prints the line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
+
+
+def solve_leg(eng, d, args, puzzles, expected, steps, warmup):
+    """Time `steps` sdk_solve_batch_dev passes over this rank's resident slice (barrier +
+    device sync on both sides, max over ranks); verify every board afterwards."""
+    n = len(puzzles)
+    d_in = eng.alloc(max(n, 1) * 81)
+    d_out = eng.alloc(max(n, 1) * 81)
+    d_st = eng.alloc(max(n, 1))
+    d_in.upload(puzzles)
+    for _ in range(warmup):
+        eng.solve_batch_dev(d_in, d_out, d_st, n)
+    eng.synchronize()
+    eng.timer_reset()
+    d.barrier()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.solve_batch_dev(d_in, d_out, d_st, n)
+    eng.synchronize()
+    d.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms, launches = eng.timer_read()
+    eng.timer_stop()
+    elapsed_max = d.max(elapsed)
+    out = np.empty((n, 81), np.uint8)
+    st = np.empty(n, np.int8)
+    d_out.download(out)
+    d_st.download(st)
+    bad = int(((out != expected).any(axis=1) | (st != 1)).sum())
+    bad_total = int(d.sum(bad))
+    for b in (d_in, d_out, d_st):
+        b.free()
+    avg_kernel_s = kernel_ms / 1000.0 / max(launches, 1)
+    return elapsed_max, avg_kernel_s, bad_total
+
+
 def main():
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     d = Dist()
+    if d.rank == 0 and d.world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={d.world}; reporting n_gpus={d.world}", file=sys.stderr)
     from distributed_sudoku_solver_amd import SudokuEngine, synth, _lib as L
+    from distributed_sudoku_solver_amd.shard import shard_bounds
 
-    eng = SudokuEngine(d.local_rank)
+    if args.engine_factory:      # CPU tests of the rank / shard logic (tests/test_bench_cpu.py)
+        import importlib
+        mod, fn = args.engine_factory.split(":")
+        eng = getattr(importlib.import_module(mod), fn)(d.local_rank)
+    else:
+        eng = SudokuEngine(d.local_rank)
     eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
-    eng.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE if args.solver == "halfwave" else L.SDK_SOLVER_WAVE)
+    eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
     if args.waves_per_cu:
-        eng.set_option(L.SDK_OPT_WAVES_PER_CU2 if args.solver == "halfwave" else L.SDK_OPT_WAVES_PER_CU,
-                       args.waves_per_cu)
-    solve_kernel = "sdk::solve2_kernel" if args.solver == "halfwave" else "sdk::solve_kernel"
+        eng.set_option(SOLVERS[args.solver][2], args.waves_per_cu)
+    solve_kernel = SOLVERS[args.solver][1]
     args.solve_kernel = solve_kernel
 
     # -------------------------------------------------------------- checker
@@ -313,15 +412,12 @@ def main():
     if args.check_boards > 0:
         nb = args.check_boards
         pool_n = min(nb, 1 << 20)
-        pool, pool_exp = synth.make_check_boards(pool_n, seed=args.seed + 7 + 1000 * d.rank)
+        pool, pool_exp = synth.make_check_boards(pool_n, seed=args.seed + 7, lo=d.rank * pool_n)
         d_b = eng.alloc(nb * 81)
         d_v = eng.alloc(nb)
         # tile the pool through HBM (content repeats; every byte is still streamed from HBM)
-        import ctypes
         for s in range(0, nb, pool_n):
-            m = min(pool_n, nb - s)
-            L.check(eng.lib.sdk_memcpy_h2d(eng.ctx, ctypes.c_void_p(d_b.ptr.value + s * 81),
-                                           ctypes.c_void_p(pool.ctypes.data), m * 81), "h2d")
+            d_b.upload(pool[:min(pool_n, nb - s)], offset=s * 81)
         for _ in range(max(1, args.check_warmup)):
             eng.check_batch_dev(d_b, d_v, nb)
         eng.synchronize()
@@ -335,6 +431,7 @@ def main():
         d.barrier()
         cel = d.max(time.perf_counter() - t0)
         cms, cl = eng.timer_read()
+        eng.timer_stop()
         v = np.empty(nb, np.uint8)
         d_v.download(v)
         reps = (nb + pool_n - 1) // pool_n
@@ -344,6 +441,7 @@ def main():
         d_v.free()
         ck_s = cms / 1000.0 / max(cl, 1)
         ach = CHECK_BYTES_PER_BOARD * nb / ck_s / 1e9
+        crec = pmc_record(args.pmc_summary, "sdk::check_kernel", nb)
         checker_leg = {
             "workload": f"C3: {nb} complete boards per GPU (50% valid), literal sudoku.py:43-94 rule",
             "value": d.world * nb * args.check_steps / cel,
@@ -351,49 +449,50 @@ def main():
             "avg_kernel_ms": ck_s * 1000.0,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBPS,
-                         "traffic": pmc_traffic(args.pmc_summary, "sdk::check_kernel")
-                         if nb == 100_000_000 else None,
+                         "traffic": crec["traffic_bytes"] if crec else None,
+                         "traffic_note": crec.get("traffic_note") if crec else None,
                          "kernel": "sdk::check_kernel"},
             "parity": {"mismatched_boards": cbad, "checked_boards": d.world * nb},
         }
 
-    # ---------------------------------------------------------------- solve
-    n = args.batch
+    # ------------------------------------------------- C4 solve (headline)
+    total = args.batch
+    lo, hi = shard_bounds(total, d.rank, d.world)
     gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
-    puzzles, expected = gen(n, seed=args.seed + 1000 * d.rank)
-    d_in = eng.alloc(n * 81)
-    d_out = eng.alloc(n * 81)
-    d_st = eng.alloc(n)
-    d_in.upload(puzzles)
+    puzzles, expected = gen(hi - lo, seed=args.seed, lo=lo)
+    n = hi - lo
+    elapsed_max, avg_kernel_s, bad_total = solve_leg(eng, d, args, puzzles, expected, args.steps, args.warmup)
 
-    for _ in range(args.warmup):
-        eng.solve_batch_dev(d_in, d_out, d_st, n)
-    eng.synchronize()
-    eng.timer_reset()
-    d.barrier()
-    eng.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.solve_batch_dev(d_in, d_out, d_st, n)
-    eng.synchronize()
-    d.barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms, launches = eng.timer_read()
-    elapsed_max = d.max(elapsed)
-
-    out = np.empty((n, 81), np.uint8)
-    st = np.empty(n, np.int8)
-    d_out.download(out)
-    d_st.download(st)
-    bad = int(((out != expected).any(axis=1) | (st != 1)).sum())
-    bad_total = int(d.sum(bad))
-    for b in (d_in, d_out, d_st):
-        b.free()
-
-    total_puzzles = d.world * n * args.steps
-    value = total_puzzles / elapsed_max
-    avg_kernel_s = kernel_ms / 1000.0 / max(launches, 1)
+    value = total * args.steps / elapsed_max
     achieved = SOLVE_BYTES_PER_PUZZLE * n / avg_kernel_s / 1e9
+    srec = pmc_record(args.pmc_summary, solve_kernel, n)
+    roofline = {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBPS,
+        "traffic": srec["traffic_bytes"] if srec else None,
+        "traffic_note": srec.get("traffic_note") if srec else None,
+        "traffic_source": (os.path.relpath(args.pmc_summary, ROOT) if srec else None),
+        "kernel": solve_kernel,
+        "avg_kernel_ms": avg_kernel_s * 1000.0,
+        "note": "the search is VALU-issue / LDS-latency bound: see roofline.valu; HBM fraction reported "
+                "per contract (163 algorithmic B per puzzle)",
+    }
+    if srec and srec.get("valu_insts"):
+        # VALU wave-instructions per launch (PMC pass of this exact launch) over the live launch time,
+        # against the issue peak: wave64 VALU issues over 2 cycles on a SIMD-32 (MI355X_MICROARCH.md)
+        peak = VALU_PEAK_WAVE_INSTR_PER_S
+        rate = srec["valu_insts"] / avg_kernel_s
+        roofline["valu"] = {
+            "bound": "valu-issue", "achieved": rate, "peak": peak, "unit": "wave-instr/s", "frac": rate / peak,
+            "valu_insts_per_puzzle": srec["valu_insts"] / n,
+            "valu_active_per_wave_cycle": srec.get("valu_active_per_wave_cycle"),
+            "lds_insts_per_puzzle": srec.get("lds_insts", 0) / n,
+            "lds_bank_conflict_cycles": srec.get("lds_bank_conflict"),
+            "source": os.path.relpath(args.pmc_summary, ROOT),
+        }
     result = {
         "metric": METRIC,
         "value": value,
@@ -403,7 +502,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed_max / args.steps * 1000.0,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
@@ -411,25 +510,15 @@ def main():
             "workload": ("C4: 17-clue hard puzzles (seeds S1-S5 x seeded Sudoku symmetries), "
                          if args.workload == "solve17" else
                          "C2: ~30-clue unique puzzles (17 seed givens + 13 solution cells, symmetries), ")
-                        + f"{n} per GPU resident in HBM",
+                        + f"{total} puzzles sharded over {d.world} GPU(s), resident in HBM",
+            "puzzles_total": total,
             "puzzles_per_gpu": n,
             "order": args.order,
-            "parallelism": f"batch-shard x{d.world} (no collectives)",
+            "solver": args.solver,
+            "parallelism": f"batch-shard x{d.world} (contiguous slices, no collectives)",
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS,
-            # the committed PMC passes ran this bench at its default sizes
-            "traffic": pmc_traffic(args.pmc_summary, solve_kernel) if n == 10_000_000 else None,
-            "traffic_source": args.pmc_summary and os.path.relpath(args.pmc_summary, ROOT),
-            "kernel": solve_kernel,
-            "avg_kernel_ms": avg_kernel_s * 1000.0,
-            "note": "search is VALU/LDS-latency bound; HBM fraction reported per contract",
-        },
-        "parity": {"mismatched_boards": bad_total, "checked_boards": d.world * n},
+        "roofline": roofline,
+        "parity": {"mismatched_boards": bad_total, "checked_boards": total},
     }
 
     if checker_leg is not None:
@@ -448,6 +537,18 @@ def main():
     dog.daemon = True
     dog.start()
 
+    # ------------------------------------------------ weak-scaling figure
+    if d.world > 1 and args.weak_leg:
+        wp, we = gen(total, seed=args.seed, lo=d.rank * total)
+        w_el, w_k, w_bad = solve_leg(eng, d, args, wp, we, args.steps, 1)
+        del wp, we
+        result["weak_scaling"] = {
+            "workload": f"C4 with {total} puzzles PER GPU (rows [rank*{total}, (rank+1)*{total}) of the same stream)",
+            "value": d.world * total * args.steps / w_el, "unit": "puzzles/s",
+            "ms_per_step": w_el / args.steps * 1000.0, "avg_kernel_ms": w_k * 1000.0,
+            "parity": {"mismatched_boards": w_bad, "checked_boards": d.world * total}}
+        bad_total += w_bad
+
     # ------------------------------------------------------------ C2 leg
     if args.c2_puzzles > 0:
         result["c2_30clue"] = c2_leg(eng, d, args, synth)
@@ -459,8 +560,11 @@ def main():
 
     # ---------------------------------------------------------- CPU baseline
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        result["cpu_baseline"] = cpu_baseline(puzzles, args.cpu_seconds, threads)
+        cores = args.cpu_cores or cpu_share()
+        # fixed C4 sample: the first 8 puzzles of every core's slice are the same on every run
+        result["cpu_baseline"] = cpu_baseline_python(puzzles[:cores * 64], args.cpu_seconds, cores,
+                                                     args.cpu_puzzle_budget, "C4 17-clue sample")
+        result["cpu_baseline_c_port"] = cpu_baseline_c(puzzles, args.cpu_seconds, cores)
 
     if d.rank == 0 and d.world == 1 and args.http_requests > 0:
         result["post_solve_latency"] = http_leg(args.http_requests)

@@ -34,6 +34,8 @@ SDK_OPT_SOLVER = 7
 SDK_OPT_WAVES_PER_CU2 = 8
 SDK_OPT_CHECK_VARIANT = 9
 SDK_OPT_SOLVE_CHUNK = 10
+SDK_OPT_TIMING = 11
+SDK_OPT_TIMER_EVENTS = 12
 SDK_CHECK_REG1 = 0
 SDK_CHECK_REG2 = 1
 SDK_CHECK_GLDS2 = 2
@@ -85,6 +87,7 @@ SIGNATURES = {
     "sdk_frontier_first_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]),
     "sdk_comm_unique_id": (ctypes.c_int, [_vp]),
     "sdk_comm_init": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
+    "sdk_comm_init_all": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     "sdk_comm_destroy": (ctypes.c_int, [_vp]),
     "sdk_comm_allreduce_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int, ctypes.c_int]),
     "sdk_comm_broadcast_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int]),

@@ -47,6 +47,8 @@ int fail(int code, const char* fmt, ...) {
                         #expr, hipGetErrorString(e_), __FILE__, __LINE__);                    \
     } while (0)
 
+constexpr size_t kMaxTimedLaunches = 1u << 16;
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -82,6 +84,7 @@ struct sdk_ctx {
     int comm_rank = 0;
     int comm_world = 1;
     // timing
+    bool timing = false;          // SDK_OPT_TIMING
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     size_t events_used = 0;
 };
@@ -99,7 +102,12 @@ int ensure(DevBuf& b, size_t bytes) {
     return SDK_OK;
 }
 
+// Kernel timing is opt-in (SDK_OPT_TIMING): with it off no event is created or
+// recorded, so a long-running node or drop-in solver holds no per-launch state.
 int timer_begin(sdk_ctx* c, hipEvent_t* stop_out) {
+    *stop_out = nullptr;
+    if (!c->timing) return SDK_OK;
+    if (c->events_used >= kMaxTimedLaunches) return fail(SDK_EINVAL, "%d timed launches since sdk_timer_reset", kMaxTimedLaunches);
     if (c->events_used == c->events.size()) {
         hipEvent_t a, b;
         HIPCALL(hipEventCreate(&a));
@@ -109,6 +117,11 @@ int timer_begin(sdk_ctx* c, hipEvent_t* stop_out) {
     auto& pr = c->events[c->events_used++];
     HIPCALL(hipEventRecord(pr.first, c->stream));
     *stop_out = pr.second;
+    return SDK_OK;
+}
+
+int timer_end(sdk_ctx* c, hipEvent_t stop) {
+    if (stop) HIPCALL(hipEventRecord(stop, c->stream));
     return SDK_OK;
 }
 
@@ -130,7 +143,7 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
         default: sdk::check_kernel<<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
     }
     HIPCALL(hipGetLastError());
-    HIPCALL(hipEventRecord(stop, c->stream));
+    if ((rc = timer_end(c, stop))) return rc;
     return SDK_OK;
 }
 
@@ -189,7 +202,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
         sdk::solve_kernel<<<grid, 64, 0, c->stream>>>(a);
     }
     HIPCALL(hipGetLastError());
-    HIPCALL(hipEventRecord(stop, c->stream));
+    if ((rc = timer_end(c, stop))) return rc;
     return SDK_OK;
 }
 
@@ -247,7 +260,7 @@ int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, i
         const uint64_t total = h[2], lvl_leaves = h[1], open = h[4];
         // level rejected: its children would not fit; fr_a stays as it is
         if (total > cap) {
-            HIPCALL(hipEventRecord(stop, c->stream));
+            if ((rc = timer_end(c, stop))) return rc;
             break;
         }
         if (total && (rc = ensure(c->fr_b, total * 81))) return rc;
@@ -259,7 +272,7 @@ int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, i
                                                        static_cast<uint8_t*>(c->fr_b.p));
             HIPCALL(hipGetLastError());
         }
-        HIPCALL(hipEventRecord(stop, c->stream));
+        if ((rc = timer_end(c, stop))) return rc;
         std::swap(c->fr_a, c->fr_b);
         m = total;
         leaves += lvl_leaves;
@@ -430,6 +443,12 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             return SDK_OK;
         case SDK_OPT_DEVICE_CUS:
             return fail(SDK_EINVAL, "SDK_OPT_DEVICE_CUS is read-only");
+        case SDK_OPT_TIMER_EVENTS:
+            return fail(SDK_EINVAL, "SDK_OPT_TIMER_EVENTS is read-only");
+        case SDK_OPT_TIMING:
+            if (value != 0 && value != 1) return fail(SDK_EINVAL, "timing must be 0 or 1");
+            c->timing = value != 0;
+            return SDK_OK;
         case SDK_OPT_SOLVER:
             if (value != SDK_SOLVER_WAVE && value != SDK_SOLVER_HALFWAVE) return fail(SDK_EINVAL, "bad solver %lld", (long long)value);
             c->solver = (int)value;
@@ -465,6 +484,8 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_WAVES_PER_CU2: *value = c->waves_per_cu2; return SDK_OK;
         case SDK_OPT_CHECK_VARIANT: *value = c->check_variant; return SDK_OK;
         case SDK_OPT_SOLVE_CHUNK: *value = c->solve_chunk; return SDK_OK;
+        case SDK_OPT_TIMING: *value = c->timing ? 1 : 0; return SDK_OK;
+        case SDK_OPT_TIMER_EVENTS: *value = (int64_t)c->events.size(); return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }
 }
@@ -651,6 +672,37 @@ int sdk_comm_init(sdk_ctx* c, const uint8_t* id, int rank, int world) {
     NCCLCALL(ncclCommInitRank(&c->comm, world, u, rank));
     c->comm_rank = rank;
     c->comm_world = world;
+    return SDK_OK;
+}
+
+int sdk_comm_init_all(const int* devices, int ndev, sdk_ctx** ctxs) {
+    if (!devices || !ctxs || ndev < 1) return fail(SDK_EINVAL, "need ndev >= 1 devices and contexts");
+    for (int k = 0; k < ndev; ++k) {
+        ctxs[k] = nullptr;
+        for (int j = 0; j < k; ++j)
+            if (devices[j] == devices[k]) return fail(SDK_EINVAL, "device %d listed twice", devices[k]);
+    }
+    int rc = SDK_OK;
+    for (int k = 0; k < ndev && rc == SDK_OK; ++k) rc = sdk_create(devices[k], &ctxs[k]);
+    std::vector<ncclComm_t> comms(ndev, nullptr);
+    if (rc == SDK_OK) {
+        const ncclResult_t r = ncclCommInitAll(comms.data(), ndev, devices);
+        if (r != ncclSuccess) rc = fail(SDK_ECOMM, "ncclCommInitAll: %s", ncclGetErrorString(r));
+    }
+    if (rc != SDK_OK) {
+        const std::string msg = g_last_error;
+        for (int k = 0; k < ndev; ++k) {
+            if (ctxs[k]) (void)sdk_destroy(ctxs[k]);
+            ctxs[k] = nullptr;
+        }
+        g_last_error = msg;
+        return rc;
+    }
+    for (int k = 0; k < ndev; ++k) {
+        ctxs[k]->comm = comms[k];
+        ctxs[k]->comm_rank = k;
+        ctxs[k]->comm_world = ndev;
+    }
     return SDK_OK;
 }
 

@@ -94,10 +94,13 @@ class DeviceBuffer:
         L.check(engine.lib.sdk_dev_alloc(engine.ctx, self.nbytes, ctypes.byref(p)), "sdk_dev_alloc")
         self.ptr = p
 
-    def upload(self, host):
+    def upload(self, host, offset=0):
+        """Copy `host` to this buffer at byte `offset`."""
         host = np.ascontiguousarray(host)
-        assert host.nbytes <= self.nbytes
-        L.check(self.engine.lib.sdk_memcpy_h2d(self.engine.ctx, self.ptr, _ptr(host), host.nbytes), "h2d")
+        if offset < 0 or offset + host.nbytes > self.nbytes:
+            raise ValueError("upload out of bounds")
+        dst = ctypes.c_void_p(self.ptr.value + int(offset))
+        L.check(self.engine.lib.sdk_memcpy_h2d(self.engine.ctx, dst, _ptr(host), host.nbytes), "h2d")
 
     def download(self, host):
         assert host.flags.c_contiguous and host.nbytes <= self.nbytes
@@ -125,6 +128,22 @@ class SudokuEngine:
             self.set_option(L.SDK_OPT_NODE_BUDGET, node_budget)
         if waves_per_cu is not None:
             self.set_option(L.SDK_OPT_WAVES_PER_CU, waves_per_cu)
+
+    @classmethod
+    def open_clique(cls, devices):
+        """One engine per device of `devices`, joined by ONE RCCL communicator made
+        in this process (sdk_comm_init_all = ncclCommInitAll); engine k is rank k.
+        Collectives must then be issued from one host thread per engine."""
+        lib = L.load()
+        devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        ctxs = (ctypes.c_void_p * len(devices))()
+        L.check(lib.sdk_comm_init_all(devs, len(devices), ctxs), f"sdk_comm_init_all({list(devices)})")
+        engines = []
+        for k, d in enumerate(devices):
+            e = cls.__new__(cls)
+            e.lib, e.ctx, e.device = lib, ctypes.c_void_p(ctxs[k]), int(d)
+            engines.append(e)
+        return engines
 
     # -------------------------------------------------------------- plumbing
     def close(self):
@@ -156,7 +175,13 @@ class SudokuEngine:
         L.check(self.lib.sdk_synchronize(self.ctx), "sdk_synchronize")
 
     def timer_reset(self):
+        """Start (or restart) kernel timing: turns SDK_OPT_TIMING on and drops old events."""
+        self.set_option(L.SDK_OPT_TIMING, 1)
         L.check(self.lib.sdk_timer_reset(self.ctx), "sdk_timer_reset")
+
+    def timer_stop(self):
+        """Stop recording kernel events (the pairs already made are kept for reuse)."""
+        self.set_option(L.SDK_OPT_TIMING, 0)
 
     def timer_read(self):
         ms = ctypes.c_double()

@@ -4,11 +4,12 @@ network work split (DHT_Node.py:491-510, utils.py:1-9).
 Puzzle and check batches are independent units: rank k (one process per GPU)
 owns the contiguous slice [k*n/G, (k+1)*n/G), runs it on its own device and the
 results are gathered to the root.  There is no collective on the data path;
-the only communication is the final gather (gloo on host memory: the results
-are already on the host after the per-GPU D2H).
+the only communication is the final gather on host memory (the results are
+already on the host after the per-GPU D2H).
 
 Two front ends:
-  * ShardedBatch: one process per GPU (torch.distributed, launched by torchrun);
+  * ShardedBatch: one process per GPU (e.g. launched by torchrun), results
+    gathered over a host transport (hostcomm.TcpComm by default);
   * MultiDeviceEngine: one process driving several GPUs from threads (ctypes
     releases the GIL for the duration of each library call).
 
@@ -26,8 +27,11 @@ and a partial board, DHT_Node.py:491-510, 225-250; utils.py:1-9):
     chunks always finish before a higher hit is accepted, so the answer is
     identical for every world size.
 The collectives go through a `comm` object: RcclComm (device memory, RCCL over
-xGMI, the product path) or HostComm (host arrays over any torch.distributed
-group, used by the CPU tests with a stand-in engine).
+xGMI, the product path), hostcomm.TcpComm (host arrays over standard-library
+sockets) or HostComm (host arrays over a torch.distributed group, CPU tests
+only).  Nothing on the product path imports torch: one process can drive every
+GPU of the node through MultiDeviceEngine.open_clique (ncclCommInitAll), and
+one process per GPU rendezvous over hostcomm.TcpComm.
 """
 import threading
 
@@ -45,35 +49,36 @@ def shard_bounds(n, rank, world):
     return (rank * n) // world, ((rank + 1) * n) // world
 
 
+def _host_transport(rank, world, comm=None, group=None):
+    """The host transport a multi-process front end uses: `comm` if given, a torch
+    group wrapped in HostComm (tests), else the standard-library TcpComm from the
+    environment (MASTER_ADDR, SDK_RDZV_PORT / MASTER_PORT + 1)."""
+    if comm is not None or world == 1:
+        return comm
+    if group is not None:
+        return HostComm(rank, world, group)
+    from .hostcomm import TcpComm
+    return TcpComm(rank, world)
+
+
 class ShardedBatch:
     """Solve / check a batch that every rank can see (e.g. generated from a shared
-    seed or read from shared storage); results are gathered on `root`."""
+    seed or read from shared storage); results are gathered on `root`.
 
-    def __init__(self, engine, rank, world, group=None, root=0):
+    The gather goes through a host transport with `gather(array, root)`:
+    hostcomm.TcpComm (standard library, the default) or HostComm (torch group)."""
+
+    def __init__(self, engine, rank, world, comm=None, group=None, root=0):
         self.engine = engine
         self.rank = rank
         self.world = world
-        self.group = group
         self.root = root
+        self.comm = _host_transport(rank, world, comm, group)
 
-    def _gather(self, local, total_shape, dtype):
+    def _gather(self, local):
         if self.world == 1:
             return local
-        import torch
-        import torch.distributed as dist
-        t = torch.from_numpy(np.ascontiguousarray(local))
-        sizes = [shard_bounds(total_shape[0], r, self.world) for r in range(self.world)]
-        if self.rank == self.root:
-            bufs = [torch.empty((hi - lo,) + tuple(total_shape[1:]), dtype=t.dtype) for lo, hi in sizes]
-            # gloo gather needs equal sizes: fall back to point-to-point receives
-            for r, (lo, hi) in enumerate(sizes):
-                if r == self.root:
-                    bufs[r] = t
-                else:
-                    dist.recv(bufs[r], src=r, group=self.group)
-            return np.concatenate([b.numpy() for b in bufs]).astype(dtype, copy=False)
-        dist.send(t, dst=self.root, group=self.group)
-        return None
+        return self.comm.gather(np.ascontiguousarray(local), self.root)
 
     def solve(self, boards, masks=None):
         boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
@@ -81,50 +86,70 @@ class ShardedBatch:
         lo, hi = shard_bounds(n, self.rank, self.world)
         m = None if masks is None else np.asarray(masks, dtype=np.uint16)[lo:hi]
         out, st, _ = self.engine.solve_batch(boards[lo:hi], m)
-        return self._gather(out, (n, 81), np.uint8), self._gather(st, (n,), np.int8)
+        return self._gather(out), self._gather(st)
 
     def check(self, boards):
         boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
         n = boards.shape[0]
         lo, hi = shard_bounds(n, self.rank, self.world)
-        v = self.engine.check_batch(boards[lo:hi])
-        return self._gather(v, (n,), np.uint8)
+        return self._gather(self.engine.check_batch(boards[lo:hi]))
+
+
+def _run_per_device(items, body):
+    """body(k, item) on one host thread per item (ctypes drops the GIL inside every
+    library call, so the devices run concurrently); first exception re-raised."""
+    errors = []
+    results = [None] * len(items)
+
+    def run(k):
+        try:
+            results[k] = body(k, items[k])
+        except BaseException as exc:  # re-raised on the caller's thread
+            errors.append(exc)
+
+    threads = [threading.Thread(target=run, args=(k,)) for k in range(len(items))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return results
 
 
 class MultiDeviceEngine:
     """Several GPUs from one process: one engine (context + stream) per device,
-    one host thread per device, disjoint output slices (no collectives)."""
+    one host thread per device.  Batches go to disjoint output slices (no
+    collectives); with `open_clique` the engines also share one RCCL communicator
+    (ncclCommInitAll, sdk_comm_init_all) for the one-board frontier searches --
+    the torch-free single-process form of SURVEY §8(e)."""
 
-    def __init__(self, engines):
+    def __init__(self, engines, comms=None):
         self.engines = list(engines)
+        self.comms = comms
 
     @classmethod
     def open(cls, devices):
         from .engine import SudokuEngine
         return cls([SudokuEngine(d) for d in devices])
 
+    @classmethod
+    def open_clique(cls, devices):
+        from .engine import SudokuEngine
+        engines = SudokuEngine.open_clique(devices)
+        n = len(engines)
+        return cls(engines, [RcclComm.attach(e, k, n) for k, e in enumerate(engines)])
+
     def close(self):
         for e in self.engines:
             e.close()
 
     def _run(self, n, work):
-        errors = []
-
-        def body(k):
-            try:
-                lo, hi = shard_bounds(n, k, len(self.engines))
-                if hi > lo:
-                    work(self.engines[k], lo, hi)
-            except BaseException as exc:  # re-raised on the caller's thread
-                errors.append(exc)
-
-        threads = [threading.Thread(target=body, args=(k,)) for k in range(len(self.engines))]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
-        if errors:
-            raise errors[0]
+        def body(k, eng):
+            lo, hi = shard_bounds(n, k, len(self.engines))
+            if hi > lo:
+                work(eng, lo, hi)
+        _run_per_device(self.engines, body)
 
     def solve_batch(self, boards, masks=None, want_work=False):
         boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
@@ -154,32 +179,61 @@ class MultiDeviceEngine:
         self._run(n, work)
         return v
 
+    # ---------------------------------- one-board searches over the clique
+    def _clique(self, fn):
+        if self.comms is None and len(self.engines) > 1:
+            raise ValueError("one-board searches over several GPUs need open_clique (an RCCL communicator)")
+        world = len(self.engines)
+        comms = self.comms or [None]
+        res = _run_per_device(self.engines, lambda k, eng: fn(eng, k, world, comms[k] if world > 1 else None))
+        return res[0]
+
+    def count(self, board, limit=0):
+        """sharded_count over every device: (total, status, frontier_size)."""
+        return self._clique(lambda e, k, w, c: sharded_count(e, board, k, w, limit=limit, comm=c))
+
+    def count_rebalanced(self, board, limit=0, info=None):
+        """sharded_count_rebalanced over every device: (total, status, frontier_size)."""
+        return self._clique(lambda e, k, w, c: sharded_count_rebalanced(e, board, k, w, limit=limit, comm=c,
+                                                                        info=info if k == 0 else None))
+
+    def solve_one(self, board, mask=None):
+        """sharded_solve over every device: the reference's answer for one board."""
+        return self._clique(lambda e, k, w, c: sharded_solve(e, board, k, w, comm=c, mask=mask))
+
 
 class RcclComm:
-    """RCCL communicator of one engine (one rank per GPU).  The 128-byte id is made
-    by rank 0 and handed to the other ranks over an existing torch.distributed
-    group (gloo is enough: it is 128 bytes once)."""
+    """RCCL communicator of one engine (one rank per GPU), collectives on device memory.
+
+    Multi-process: rank 0 makes the 128-byte id and a host transport hands it to
+    the other ranks once (`transport.broadcast_bytes`; hostcomm.TcpComm by
+    default, or a torch group through HostComm in tests).  Single process: the
+    engines of SudokuEngine.open_clique already share a communicator (attach)."""
 
     _DT = {np.dtype(np.uint64): L.SDK_COMM_U64, np.dtype(np.int64): L.SDK_COMM_I64,
            np.dtype(np.uint8): L.SDK_COMM_U8}
     _OP = {"sum": L.SDK_COMM_SUM, "min": L.SDK_COMM_MIN, "max": L.SDK_COMM_MAX}
 
-    def __init__(self, engine, rank, world, group=None, uid=None):
+    def __init__(self, engine, rank, world, group=None, uid=None, transport=None, _attach=False):
         self.engine, self.rank, self.world = engine, rank, world
+        if _attach:
+            return
         if uid is None:
-            uid = self.exchange_id(rank, group)
+            uid = self.exchange_id(rank, _host_transport(rank, world, transport, group) if world > 1 else None)
         engine.comm_init(uid, rank, world)
 
+    @classmethod
+    def attach(cls, engine, rank, world):
+        """Wrap an engine whose context already has a communicator (open_clique)."""
+        return cls(engine, rank, world, _attach=True)
+
     @staticmethod
-    def exchange_id(rank, group=None):
-        import torch
-        import torch.distributed as dist
+    def exchange_id(rank, transport):
         from .engine import SudokuEngine
-        t = torch.zeros(L.SDK_COMM_ID_BYTES, dtype=torch.uint8)
-        if rank == 0:
-            t[:] = torch.frombuffer(bytearray(SudokuEngine.comm_unique_id()), dtype=torch.uint8)
-        dist.broadcast(t, src=0, group=group)
-        return bytes(t.numpy().tobytes())
+        uid = SudokuEngine.comm_unique_id() if rank == 0 else None
+        if transport is None:
+            return uid
+        return transport.broadcast_bytes(uid, 0)
 
     def allreduce(self, buf, count, dtype, op):
         self.engine.comm_allreduce(buf, count, self._DT[np.dtype(dtype)], self._OP[op])
@@ -196,7 +250,8 @@ class RcclComm:
 
 class HostComm:
     """Same interface over host numpy arrays and a torch.distributed group (gloo):
-    the CPU stand-in for RcclComm in multi-process tests."""
+    the CPU stand-in for RcclComm in multi-process tests (torch is imported only
+    here, never on the product path)."""
 
     _OPS = {"sum": "SUM", "min": "MIN", "max": "MAX"}
 
@@ -224,6 +279,41 @@ class HostComm:
         parts = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(parts, t, group=self.group)
         recv.view(np.uint8)[:self.world * nbytes] = torch.cat(parts).numpy()
+
+    def broadcast_bytes(self, data, root=0):
+        import torch
+        import torch.distributed as dist
+        n = torch.tensor([len(data) if self.rank == root else 0], dtype=torch.int64)
+        dist.broadcast(n, src=root, group=self.group)
+        t = torch.zeros(int(n.item()), dtype=torch.uint8)
+        if self.rank == root:
+            t[:] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        dist.broadcast(t, src=root, group=self.group)
+        return bytes(t.numpy().tobytes())
+
+    def gather(self, local, root=0):
+        """Row-concatenation at `root` (gloo gather needs equal sizes: point-to-point)."""
+        import torch
+        import torch.distributed as dist
+        local = np.ascontiguousarray(local)
+        n = torch.tensor([local.shape[0]], dtype=torch.int64)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
+        dist.all_gather(sizes, n, group=self.group)
+        row = local.dtype.itemsize * int(np.prod(local.shape[1:], dtype=np.int64))
+        if self.rank != root:
+            if local.shape[0]:
+                dist.send(torch.from_numpy(local.view(np.uint8).reshape(-1).copy()), dst=root, group=self.group)
+            return None
+        parts = []
+        for r in range(self.world):
+            k = int(sizes[r].item())
+            if r == root:
+                parts.append(local)
+            elif k:
+                buf = torch.empty(k * row, dtype=torch.uint8)
+                dist.recv(buf, src=r, group=self.group)
+                parts.append(buf.numpy().view(local.dtype).reshape((k,) + local.shape[1:]))
+        return np.concatenate(parts)
 
     def close(self):
         pass

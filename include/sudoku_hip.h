@@ -72,6 +72,9 @@ extern "C" {
 #define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE solver per CU, 1..32 (default 32) */
 #define SDK_OPT_CHECK_VARIANT 9 /* checker tile pipeline: SDK_CHECK_* (default REG1) */
 #define SDK_OPT_SOLVE_CHUNK  10  /* boards per solver dequeue, 0 = automatic (default)  */
+#define SDK_OPT_TIMING       11  /* 1 = bracket every kernel with HIP events for        */
+                                 /* sdk_timer_read (default 0: no events are created)    */
+#define SDK_OPT_TIMER_EVENTS 12  /* read-only: HIP event pairs the context holds         */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */
@@ -176,6 +179,12 @@ int sdk_frontier_first_dev(sdk_ctx *ctx, uint64_t lo, uint64_t hi, void *d_found
 #define SDK_COMM_MAX 2
 int sdk_comm_unique_id(uint8_t *id /* SDK_COMM_ID_BYTES */);
 int sdk_comm_init(sdk_ctx *ctx, const uint8_t *id, int rank, int world);
+/* Single-process form: creates one context per device of
+ * `devices` (distinct GPUs) and ONE RCCL clique over them (ncclCommInitAll);
+ * ctxs[k] is rank k.  Collectives on the contexts must then be issued from one
+ * host thread per context (each call enqueues on its own stream).  On failure
+ * no context is left behind (ctxs[k] = NULL).  Release with sdk_destroy. */
+int sdk_comm_init_all(const int *devices, int ndev, sdk_ctx **ctxs);
 int sdk_comm_destroy(sdk_ctx *ctx);
 /* In place, on device memory, enqueued on the context stream. */
 int sdk_comm_allreduce_dev(sdk_ctx *ctx, void *d_buf, size_t count, int dtype, int op);
@@ -196,8 +205,9 @@ int sdk_solve_batch_dev(sdk_ctx *ctx, const void *d_in, const void *d_first_cell
                         void *d_out, void *d_status, void *d_work, size_t n);
 
 /* Kernel time accounting (HIP events on the context stream, bracketing every
- * kernel launched by the *_dev / host calls since the last reset).  Valid
- * after sdk_synchronize. */
+ * kernel launched by the *_dev / host calls since the last reset).  Only with
+ * SDK_OPT_TIMING = 1; at most 65536 timed launches between resets (further
+ * launches fail with SDK_EINVAL).  Valid after sdk_synchronize. */
 int sdk_timer_reset(sdk_ctx *ctx);
 int sdk_timer_read(sdk_ctx *ctx, double *total_ms, int64_t *launches);
 

@@ -111,10 +111,15 @@ def check_batch(boards, threads=1):
 
 
 # --------------------------------------------------------------- pure Python
-def py_naive_solve(cells, lo=1, hi=10):
+class _Budget(Exception):
+    pass
+
+
+def py_naive_solve(cells, lo=1, hi=10, budget=0):
     """Line-by-line Python restatement of DHTNode.solve_sudoku (DHT_Node.py:474-538),
     with find_next_empty (utils.py:14-25) and is_valid (utils.py:27-56) inlined.
-    Returns (ok, board, validations).  Small cases only."""
+    Returns (ok, board, validations); ok is None when `budget` (> 0) validations
+    were spent first (the per-puzzle timeout of the cpu_baseline leg).  Small cases only."""
     grid = [list(cells[9 * r: 9 * r + 9]) for r in range(9)]
     counter = [0]
 
@@ -139,6 +144,8 @@ def py_naive_solve(cells, lo=1, hi=10):
 
     def solve(arr):
         counter[0] += 1                      # DHT_Node.py:513
+        if budget and counter[0] > budget:
+            raise _Budget()
         row, col = find_next_empty()
         if row is None:
             return True
@@ -151,7 +158,10 @@ def py_naive_solve(cells, lo=1, hi=10):
             grid[row][col] = 0               # DHT_Node.py:535
         return False
 
-    ok = solve(range(lo, hi))
+    try:
+        ok = solve(range(lo, hi))
+    except _Budget:
+        return None, list(cells), counter[0]
     return ok, [v for row in grid for v in row], counter[0]
 
 
@@ -172,17 +182,19 @@ def py_check(cells):
     return raw, bool(boxes)
 
 
-def py_solve_timed(boards, seconds):
+def py_solve_timed(boards, seconds, budget=0):
     """Baseline worker (bench.py cpu_baseline leg): the Python restatement above on
-    `boards` (list of 81-int lists) one after another until `seconds` have passed.
-    Returns (done, solved, wall_s)."""
+    `boards` (list of 81-int lists) one after another until `seconds` have passed,
+    each puzzle capped at `budget` validations (0 = none).
+    Returns (done, solved, wall_s, timeouts)."""
     import time
     t0 = time.perf_counter()
-    done = solved = 0
+    done = solved = timeouts = 0
     for cells in boards:
         if time.perf_counter() - t0 >= seconds:
             break
-        ok, _, _ = py_naive_solve(cells)
+        ok, _, _ = py_naive_solve(cells, budget=budget)
         done += 1
-        solved += int(ok)
-    return done, solved, time.perf_counter() - t0
+        solved += int(bool(ok))
+        timeouts += int(ok is None)
+    return done, solved, time.perf_counter() - t0, timeouts

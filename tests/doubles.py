@@ -1,0 +1,149 @@
+"""Test doubles shared by the CPU multi-process tests (no torch here)."""
+import numpy as np
+
+from distributed_sudoku_solver_amd import _lib as L
+
+
+class OracleEngine:
+    """Test double with the SudokuEngine batch interface, computed by the oracle."""
+
+    def __init__(self):
+        from oracle import oracle as O
+        self.O = O
+        self.calls = []
+
+    def solve_batch(self, boards, masks=None, want_work=False):
+        self.calls.append(len(boards))
+        out, st, val = self.O.naive_solve_batch(boards, masks, budget=50_000_000, threads=2)
+        return out, st, (val if want_work else None)
+
+    def check_batch(self, boards):
+        self.calls.append(len(boards))
+        return self.O.check_batch(boards, threads=2)
+
+    # ---- frontier primitives, restated on the CPU (test double of libsudoku_hip's) ----
+    def get_option(self, key):
+        return {L.SDK_OPT_DEVICE_CUS: 1, L.SDK_OPT_WAVES_PER_CU: 2}[key]
+
+    def frontier_build(self, board, mask=None, mode=L.SDK_FRONTIER_COUNT, target=0):
+        """Naive-DFS order expansion (lowest empty cell, digits ascending, utils.py:14-56)
+        without propagation, level by level until >= target boards."""
+        fr = [np.asarray(board, dtype=np.uint8).copy()]
+        allowed0 = mask
+        while fr and len(fr) < max(target, 1):
+            nxt, grew = [], False
+            for b in fr:
+                z = np.flatnonzero(b == 0)
+                if len(z) == 0:
+                    nxt.append(b)
+                    continue
+                grew = True
+                c = int(z[0])
+                r, col = divmod(c, 9)
+                br, bc = 3 * (r // 3), 3 * (col // 3)
+                used = set(b[9 * r: 9 * r + 9]) | set(b[col::9]) | {b[9 * (br + i) + bc + j] for i in range(3)
+                                                                    for j in range(3)}
+                for d in range(1, 10):
+                    if allowed0 is not None and not (allowed0 >> d) & 1:
+                        continue
+                    if d not in used:
+                        ch = b.copy()
+                        ch[c] = d
+                        nxt.append(ch)
+            allowed0 = None
+            fr = nxt
+            if not grew:
+                break
+        self.frontier = fr
+        return len(fr), 0
+
+    def result_buffer(self, count, dtype):
+        return np.zeros(count, dtype=dtype)
+
+    def read(self, buf, count, dtype):
+        return buf[:count].astype(dtype)
+
+    def frontier_count(self, first, step, end, limit, res):
+        idx = list(range(first, min(end, len(self.frontier)), step))
+        self.calls.append(("count", idx))
+        res[0] = sum(self.O.count(self.frontier[i], limit, 1) for i in idx)
+        res[1] = 0
+
+    def frontier_first(self, lo, hi, found, best):
+        hi = min(hi, len(self.frontier))
+        self.calls.append(("first", lo, hi))
+        found[0] = (1 << 63) - 1
+        if hi > lo:
+            out, st, _ = self.O.naive_solve_batch(np.stack(self.frontier[lo:hi]), budget=50_000_000, threads=2)
+            hits = np.flatnonzero(st != 0)
+            if len(hits):
+                i = int(hits[0])
+                found[0] = lo + i
+                best[:81] = out[i]
+                best[81] = np.int8(st[i]).view(np.uint8)
+
+
+class _HostBuffer:
+    """Host stand-in for engine.DeviceBuffer."""
+
+    def __init__(self, nbytes):
+        self.data = np.zeros(int(nbytes), dtype=np.uint8)
+
+    def upload(self, host, offset=0):
+        raw = np.ascontiguousarray(host).view(np.uint8).reshape(-1)
+        self.data[offset:offset + raw.size] = raw
+
+    def download(self, host):
+        raw = host.view(np.uint8).reshape(-1)
+        raw[:] = self.data[:raw.size]
+        return host
+
+    def free(self):
+        self.data = None
+
+
+class BenchStubEngine:
+    """The device-buffer interface bench.py drives, computed by the oracle on the host:
+    lets the CPU tests run bench.py's rank launcher and sharding logic (no GPU here)."""
+
+    def __init__(self, device=0):
+        from oracle import oracle as O
+        self.O = O
+        self.device = device
+        self.opts = {}
+        self.launches = 0
+
+    def set_option(self, key, value):
+        self.opts[key] = int(value)
+
+    def get_option(self, key):
+        return self.opts.get(key, 0)
+
+    def alloc(self, nbytes):
+        return _HostBuffer(nbytes)
+
+    def solve_batch_dev(self, d_in, d_out, d_st, n, d_mask=None, d_work=None):
+        boards = d_in.data[:n * 81].reshape(n, 81)
+        out, st, _ = self.O.naive_solve_batch(boards, budget=50_000_000, threads=2)
+        d_out.data[:n * 81] = out.reshape(-1)
+        d_st.data[:n] = st.view(np.uint8)
+        self.launches += 1
+
+    def check_batch_dev(self, d_b, d_v, n):
+        d_v.data[:n] = self.O.check_batch(d_b.data[:n * 81].reshape(n, 81), threads=2)
+        self.launches += 1
+
+    def synchronize(self):
+        pass
+
+    def timer_reset(self):
+        self.launches = 0
+
+    def timer_read(self):
+        return 1e-3 * max(self.launches, 1), self.launches
+
+    def timer_stop(self):
+        pass
+
+    def close(self):
+        pass

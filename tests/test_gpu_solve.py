@@ -338,3 +338,47 @@ def test_dequeue_chunk_override(engine, chunk):
             assert (st == 1).all() and (out == s[:n]).all(), (chunk, n)
     finally:
         engine.set_option(L.SDK_OPT_SOLVE_CHUNK, 0)
+
+
+def test_clique_single_process_rccl():
+    """sdk_comm_init_all (ncclCommInitAll) at ndev = 1: the torch-free single-process
+    multi-GPU path runs the frontier searches through its own communicator."""
+    from distributed_sudoku_solver_amd.shard import MultiDeviceEngine
+    mde = MultiDeviceEngine.open_clique([0])
+    try:
+        s1 = synth.SEEDS17["S1"]
+        assert mde.count(synth.parse(s1[:-9] + "0" * 9))[:2] == (3481026, 1)
+        info = {}
+        assert mde.count_rebalanced(synth.parse(s1[:-9] + "000800000"), info=info)[:2] == (7309, 1)
+        out, st = mde.solve_one(synth.parse(DEMO))
+        assert st == 1 and "".join(map(str, out)) == \
+            "234156789179328456568479132391245678425687391687913245752831964816794523943562817"
+        p, s = synth.make_17clue(5000, seed=3)
+        o, st, _ = mde.solve_batch(p)
+        assert (st == 1).all() and (o == s).all()
+    finally:
+        mde.close()
+
+
+def test_timing_is_opt_in():
+    """Without SDK_OPT_TIMING no HIP events are made, however many launches run."""
+    eng = SudokuEngine(0)
+    try:
+        p, s = synth.make_17clue(64, seed=4)
+        for _ in range(200):
+            eng.solve_batch(p)
+            eng.check_batch(s)
+        assert eng.get_option(L.SDK_OPT_TIMER_EVENTS) == 0
+        eng.timer_reset()
+        for _ in range(3):
+            eng.solve_batch(p)
+        ms, n = eng.timer_read()
+        assert n == 3 and ms > 0 and eng.get_option(L.SDK_OPT_TIMER_EVENTS) == 3
+        eng.timer_reset()
+        eng.solve_batch(p)
+        assert eng.timer_read()[1] == 1 and eng.get_option(L.SDK_OPT_TIMER_EVENTS) == 3   # pairs reused
+        eng.timer_stop()
+        eng.solve_batch(p)
+        assert eng.timer_read()[1] == 1
+    finally:
+        eng.close()

@@ -24,8 +24,23 @@ What changes (GPU-first):
     puzzle answers 201 {"solution": null} instead of hanging.
   * `-d/--delay` keeps its role as a slow-node knob: milliseconds per search
     node spent by the engine (the reference sleeps per guess, DHT_Node.py:524).
+  * Work splitting (DHT_Node.py:491-510): when the neighbour is free, a queued
+    TASK is handed over whole (at NEEDWORK time, or when a TASK arrives while
+    this node is busy); otherwise the next task's digit `range` is halved with
+    split_array_in_middle (utils.py:1-9) just before the launch.  Unlike the
+    reference, the node keeps the LOWER half and sends the upper half: its own
+    half is solved in microseconds, so the lexicographically first completion
+    (the single-node answer) is the one reported first.
+  * A task without a completion is reported back: NO_SOLUTION {uuid, range,
+    sudoku} to its `initial_node` (a new method; reference nodes ignore it).
+    The HTTP origin answers 201 {"solution": null} once the failed ranges of
+    its puzzle cover every digit, instead of hanging.
+  * api="main" serves main.py's HTTP surface instead (main.py:356-406): POST
+    /solve -> 201 {"solution"}; GET /stats (local counters only); GET /network
+    -> {"node": "h:p", "predecessor": [h, p] | null, "neighbor": [h, p] | null}.
 """
 import argparse
+import collections
 import io
 import json
 import pickle
@@ -38,7 +53,8 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 import numpy as np
 
-from .engine import encode_solve_grid, range_to_mask
+from .engine import ALL_DIGITS_MASK, encode_solve_grid, range_to_mask
+from .utils import split_array_in_middle
 from . import _lib as L
 
 RECV_BYTES = 1024          # DHT_Node.py:82,94
@@ -74,7 +90,12 @@ class SudokuNode:
     """One ring member.  `engine` is a SudokuEngine (or anything with solve_batch)."""
 
     def __init__(self, host, p2p_port, http_port, anchor=None, engine=None, delay_ms=0.0,
-                 heartbeat_s=HEARTBEAT_S, stats_wait_s=STATS_WAIT_S, solve_timeout_s=600.0, log=False):
+                 heartbeat_s=HEARTBEAT_S, stats_wait_s=STATS_WAIT_S, solve_timeout_s=600.0, log=False,
+                 api="dht", split=True, trace=False):
+        if api not in ("dht", "main"):
+            raise ValueError("api must be 'dht' (DHT_Node.py) or 'main' (main.py)")
+        self.api = api
+        self.split = split
         self.host = host
         self.port = p2p_port
         self.http_port = http_port
@@ -103,7 +124,8 @@ class SudokuNode:
         self.neighbor_tasks = []                 # tasks handed to the neighbour (re-run on its failure)
         self.busy = False
         self.done_uuids = set()                  # uuids already solved somewhere in the ring
-        self.waiters = {}                        # uuid -> (Event, [solution])
+        self.waiters = {}                        # uuid -> (Event, [solution], puzzle, failed digit mask)
+        self.trace = collections.deque(maxlen=4096) if trace else None   # (method, addr, range) sent
         self.validations = 0
         self.solved_count = 0
         self.stats_replies = {}
@@ -126,6 +148,8 @@ class SudokuNode:
             print(f"[node {self.port}]", *a, flush=True)
 
     def send(self, msg, addr):
+        if self.trace is not None:
+            self.trace.append((msg.get("method"), _addr(addr), msg.get("range")))
         try:
             self.sock.sendto(encode_datagram(msg), _addr(addr))
         except OSError as e:
@@ -198,6 +222,11 @@ class SudokuNode:
         fn(msg)
 
     def _on_TASK(self, msg):
+        try:
+            _validate_task(msg)
+        except (KeyError, TypeError, ValueError) as e:     # the reference catches per message too
+            self._log("dropped malformed TASK:", e)
+            return
         self.enqueue(msg)
 
     def _on_NEEDWORK(self, msg):
@@ -276,9 +305,13 @@ class SudokuNode:
         uid = msg.get("uuid")
         with self.lock:
             self.solved_count += 1
-            self.done_uuids.add(uid)
-            self._purge(uid)
+            if uid is not None:
+                self.done_uuids.add(uid)
+                self._purge(uid)
         self._wake(uid, msg.get("solution"))
+
+    def _on_NO_SOLUTION(self, msg):
+        self._failed(msg.get("uuid"), msg.get("range"), msg.get("sudoku"))
 
     def _on_STATS_REQ(self, msg):
         with self.lock:
@@ -339,6 +372,10 @@ class SudokuNode:
     # --------------------------------------------------------- task execution
     def enqueue(self, task):
         self.tasks.put(task)
+        with self.lock:
+            busy = self.busy
+        if busy:                 # an idle neighbour takes what would wait behind the running batch
+            self._maybe_delegate()
         with self._work:
             self._work.notify()
 
@@ -379,17 +416,48 @@ class SudokuNode:
             with self.lock:
                 batch = [t for t in self._drain_queue() if t.get("uuid") not in self.done_uuids]
                 self.busy = True
-            if batch:
-                self._run_batch(batch)
-            with self.lock:
-                self.busy = False
-                pred = self.predecessor
-                idle = self.tasks.empty()
+            try:
+                if batch:
+                    self._run_batch(batch)
+            except Exception as e:      # the worker must survive a failed launch
+                self._log("batch failed:", repr(e))
+                for t in batch:
+                    self._wake(t.get("uuid"), None, error=repr(e))
+            finally:
+                with self.lock:
+                    self.busy = False
+                    pred = self.predecessor
+                    idle = self.tasks.empty()
             if idle and pred and pred != self.me:
                 self.send({"method": "NEEDWORK"}, pred)        # DHT_Node.py:245-248
 
+    def _split_for_neighbor(self, batch):
+        """DHT_Node.py:491-510 at launch time: a free neighbour gets the upper half of the
+        first splittable task's digit range (split_array_in_middle, utils.py:1-9); this node
+        keeps the lower half, so its own (first reported) answer stays the lex-first one."""
+        if not self.split:
+            return
+        with self.lock:
+            if not (self.neighborfree and self.neighbor and self.neighbor != self.me):
+                return
+            for i, t in enumerate(batch):
+                arr = t.get("range", range(1, 10))
+                if len(arr) < 2:
+                    continue
+                lower, upper = split_array_in_middle(arr)
+                half = dict(t, range=upper)
+                batch[i] = dict(t, range=lower)
+                self.neighborfree = False
+                self.neighbor_tasks.append(half)
+                nb = self.neighbor
+                break
+            else:
+                return
+        self.send(half, nb)
+
     def _run_batch(self, batch):
         """All queued TASKs in one sdk_solve_batch launch."""
+        self._split_for_neighbor(batch)
         boards = np.stack([encode_solve_grid(t["sudoku"]) for t in batch])
         masks = np.array([range_to_mask(t.get("range", range(1, 10))) for t in batch], dtype=np.uint16)
         out, status, work = self.engine.solve_batch(boards, masks, want_work=True)
@@ -406,32 +474,57 @@ class SudokuNode:
                     for c in range(9):
                         if grid[r][c] == 0:
                             grid[r][c] = int(o[9 * r + c])
-                self._solved(uid, grid)
-            elif st == L.SDK_BUDGET_HIT:
-                self._log("budget exhausted for", uid)
+                self._solved(uid, grid, t.get("initial_node"))
             else:
-                # this task's digit range has no completion; when the task is the
-                # whole puzzle (HTTP origin) the answer is "no solution"
-                if t.get("initial_node") is not None and _is_full_range(t.get("range")):
-                    self._wake(uid, None)
+                if st == L.SDK_BUDGET_HIT:
+                    self._log("budget exhausted for", uid)
+                # this task's digit range has no completion (or none within the budget): tell
+                # the HTTP origin, which answers once its puzzle's failed ranges cover 1..9
+                origin = _addr(t.get("initial_node"))
+                if origin is None or origin == self.me:
+                    self._failed(uid, t.get("range"), t["sudoku"])
+                else:
+                    self.send({"method": "NO_SOLUTION", "uuid": uid, "range": t.get("range", range(1, 10)),
+                               "sudoku": t["sudoku"], "node": self.me}, origin)
 
-    def _solved(self, uid, grid):
+    def _solved(self, uid, grid, origin=None):
         with self.lock:
-            if uid in self.done_uuids:
-                return
-            self.done_uuids.add(uid)
+            if uid is not None:              # main.py TASKs carry no uuid (main.py:359-360)
+                if uid in self.done_uuids:
+                    return
+                self.done_uuids.add(uid)
+                self._purge(uid)
             self.solved_count += 1
-            self._purge(uid)
             peers = [n for n in self.network if n != self.me]
+        origin = _addr(origin)
+        if origin is not None and origin != self.me and origin not in peers:
+            peers.append(origin)
         for node in peers:
             self.send({"method": "SOLUTION_FOUND", "solution": grid, "node": self.me, "uuid": uid}, node)
         self._wake(uid, grid)
 
-    def _wake(self, uid, solution):
+    def _failed(self, uid, arr, sudoku):
+        """A range of puzzle `uid` has no completion: wake its HTTP waiter once every digit of
+        the first empty cell has failed (only reports about the waiter's own board count)."""
+        try:
+            m = range_to_mask(arr if arr is not None else range(1, 10))
+            board = encode_solve_grid(sudoku)
+        except (TypeError, ValueError):
+            return
+        with self.lock:
+            w = self.waiters.get(uid)
+            if w is None or not np.array_equal(w[2], board):
+                return
+            w[3][0] |= m
+            done = (w[3][0] & ALL_DIGITS_MASK) == ALL_DIGITS_MASK
+        if done:
+            self._wake(uid, None)
+
+    def _wake(self, uid, solution, error=None):
         with self.lock:
             w = self.waiters.get(uid)
         if w is not None:
-            w[1].append(solution)
+            w[1].append(solution if error is None else _Failure(error))
             w[0].set()
 
     # ------------------------------------------------------------- HTTP side
@@ -439,16 +532,20 @@ class SudokuNode:
         uid = uuidlib.uuid4()
         ev = threading.Event()
         box = []
+        task = {"method": "TASK", "sudoku": puzzle, "range": range(1, 10), "uuid": uid, "initial_node": self.me}
+        _validate_task(task)
         with self.lock:
-            self.waiters[uid] = (ev, box)
-        self.enqueue({"method": "TASK", "sudoku": puzzle, "range": range(1, 10), "uuid": uid,
-                      "initial_node": self.me})
+            self.waiters[uid] = (ev, box, encode_solve_grid(puzzle), [0])
+        self.enqueue(task)
         ok = ev.wait(self.solve_timeout_s)
         with self.lock:
             self.waiters.pop(uid, None)
         if not ok:
             raise TimeoutError("no solution reported in time")
-        return box[0] if box else None
+        res = box[0] if box else None
+        if isinstance(res, _Failure):
+            raise RuntimeError(f"solve failed: {res.error}")
+        return res
 
     def stats(self):
         with self.lock:
@@ -470,6 +567,19 @@ class SudokuNode:
         nodes += [{"address": a, "validation": v} for a, v in replies.items()]   # reference key, DHT_Node.py:591
         return {"all": {"solved": solved, "validations": mine + sum(replies.values())}, "nodes": nodes}
 
+    def stats_local(self):
+        """main.py's /stats: this node's counters only (main.py:378-395)."""
+        with self.lock:
+            return {"all": {"solved": self.solved_count, "validations": int(self.validations)},
+                    "nodes": [{"address": f"{self.host}:{self.port}", "validations": int(self.validations)}]}
+
+    def network_view_main(self):
+        """main.py's /network (main.py:397-406): tuples serialise as JSON lists."""
+        with self.lock:
+            pred = None if self.predecessor is None else list(self.predecessor)
+            nb = None if self.neighbor is None else list(self.neighbor)
+        return {"node": f"{self.host}:{self.port}", "predecessor": pred, "neighbor": nb}
+
     def network_view(self):
         with self.lock:
             net = list(self.network)
@@ -477,11 +587,15 @@ class SudokuNode:
         return {str(a): [str(net[(i - 1) % n]), str(net[(i + 1) % n])] for i, a in enumerate(net)}
 
 
-def _is_full_range(r):
-    try:
-        return range_to_mask(r if r is not None else range(1, 10)) == 0x3FE
-    except ValueError:
-        return False
+class _Failure:
+    def __init__(self, error):
+        self.error = error
+
+
+def _validate_task(msg):
+    """Raise unless a TASK can be launched: a 9x9 (or flat 81) grid and an ascending 0..9 range."""
+    encode_solve_grid(msg["sudoku"])
+    range_to_mask(msg.get("range", range(1, 10)))
 
 
 class _Handler(BaseHTTPRequestHandler):
@@ -512,13 +626,21 @@ class _Handler(BaseHTTPRequestHandler):
             solution = node.solve_http(puzzle)
         except TimeoutError as e:
             return self._reply(504, {"error": str(e)})
+        except (ValueError, TypeError) as e:
+            return self._reply(400, {"error": str(e)})
+        except RuntimeError as e:
+            return self._reply(500, {"error": str(e)})
+        if node.api == "main":                                  # main.py:375
+            return self._reply(201, {"solution": solution})
         self._reply(201, {"solution": solution, "duration": time.time() - t0})
 
     def do_GET(self):
         node = self.server.node
         if self.path == "/stats":
-            return self._reply(200, node.stats())
+            return self._reply(200, node.stats_local() if node.api == "main" else node.stats())
         if self.path == "/network":
+            if node.api == "main":
+                return self._reply(200, node.network_view_main())
             return self._reply(200, node.network_view(), indent=4)
         self._reply(404, {"error": "not found"})
 
@@ -531,13 +653,15 @@ def main(argv=None):
     ap.add_argument("-d", "--delay", type=float, default=1.0, help="ms per engine search node (slow-node knob)")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--api", choices=["dht", "main"], default="dht", help="HTTP surface: DHT_Node.py or main.py")
     args = ap.parse_args(argv)
     anchor = None
     if args.anchor:
         h, p = args.anchor.rsplit(":", 1)
         anchor = (h, int(p))
     from .engine import SudokuEngine
-    node = SudokuNode(args.host, args.p2p_port, args.port, anchor, SudokuEngine(args.device), args.delay, log=True)
+    node = SudokuNode(args.host, args.p2p_port, args.port, anchor, SudokuEngine(args.device), args.delay, log=True,
+                      api=args.api)
     node.start()
     try:
         while True:

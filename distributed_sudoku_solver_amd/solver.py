@@ -76,6 +76,8 @@ class HipSolveMixin:
         data, addr = self.non_blocking_receive()              # DHT_Node.py:485-488
         if data:
             self.handleMessage(data, addr)
+            if self.task == []:      # the poll may have cancelled this task (SOLUTION_FOUND, DHT_Node.py:348-387)
+                return False
         if self.neighbor and self.neighborfree:               # DHT_Node.py:491-510
             if not self.task_queue.empty():
                 task = self.task_queue.get()
@@ -104,6 +106,8 @@ class HipSolveMixinMain:
         data, addr = self.non_blocking_receive()              # main.py:308-311
         if data:
             self.handleMessage(data, addr)
+            if self.task == []:
+                return False
         if self.neighbor and self.neighborfree and len(arr) > 1:   # main.py:313-325
             first_half, arr = split_array_in_middle(arr)
             self.send_data({"method": "TASK", "sudoku": puzzle, "range": first_half}, self.neighbor)

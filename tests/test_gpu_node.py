@@ -44,3 +44,91 @@ def test_gpu_ring(engine):
         assert len(st["nodes"]) == 3 and st["all"]["solved"] >= 3
     finally:
         _stop(nodes)
+
+
+class _Counting:
+    """Counts engine launches of the HIP engine (one sdk_solve_batch per call)."""
+
+    def __init__(self, eng):
+        self.eng, self.sizes = eng, []
+
+    def solve_batch(self, boards, masks=None, want_work=False):
+        self.sizes.append(len(boards))
+        return self.eng.solve_batch(boards, masks, want_work)
+
+
+def test_concurrent_posts_batch_into_few_launches(engine):
+    """SURVEY §8(f)2 / DHT_Node.py:225-250: 64 concurrent POST /solve on one node are drained into
+    a few sdk_solve_batch launches, and every answer is the reference's solution."""
+    import threading
+    from distributed_sudoku_solver_amd import synth as S
+    ce = _Counting(engine)
+    node = SudokuNode("127.0.0.1", 0, 0, engine=ce, delay_ms=0).start()
+    try:
+        p, s = S.make_17clue(64, seed=123)
+        res = [None] * 64
+        with node.lock:
+            node.busy = True               # hold the worker until every request is queued
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, _post(node.http_port, _grid("".join(map(str, p[i]))))))
+               for i in range(64)]
+        for t in ths:
+            t.start()
+        t0 = time.time()
+        while node.tasks.qsize() < 64 and time.time() - t0 < 30:
+            time.sleep(0.01)
+        with node.lock:
+            node.busy = False
+        with node._work:
+            node._work.notify()
+        for t in ths:
+            t.join(60)
+        for i in range(64):
+            assert res[i][0] == 201
+            assert "".join(str(v) for row in res[i][1]["solution"] for v in row) == "".join(map(str, s[i]))
+        assert sum(ce.sizes) == 64 and len(ce.sizes) <= 4, ce.sizes
+    finally:
+        _stop([node])
+
+
+def test_mixed_ring_split_returns_golden(engine):
+    """§8(f)3: a HIP node and an oracle-backed node; the HIP node halves the demo board's digit
+    range for its free neighbour (DHT_Node.py:491-510) and the answer is the reference's golden."""
+    from test_node import DEMO8, DEMO8_FIRST, OracleEngine
+    a = SudokuNode("127.0.0.1", 0, 0, engine=engine, delay_ms=0, trace=True).start()
+    b = SudokuNode("127.0.0.1", 0, 0, anchor=a.me, engine=OracleEngine(), delay_ms=0, trace=True).start()
+    try:
+        assert b.wait_joined()
+        t0 = time.time()
+        while not a.neighborfree and time.time() - t0 < 5:
+            time.sleep(0.01)
+        code, body = _post(a.http_port, _grid(DEMO8))
+        assert code == 201 and "".join(str(v) for row in body["solution"] for v in row) == DEMO8_FIRST
+        assert [t for t in a.trace if t[0] == "TASK"][0][1:] == (b.me, range(5, 10))
+        # a unique puzzle whose answer lies in the neighbour's half
+        code, body = _post(a.http_port, _grid(synth.SEEDS17["S1"]))
+        assert "".join(str(v) for row in body["solution"] for v in row) == synth.SEED_SOLUTIONS["S1"]
+    finally:
+        _stop([a, b])
+
+
+def test_main_api_and_main_mixin_on_gpu(engine, solve_cases):
+    from distributed_sudoku_solver_amd.solver import HipSolveMixinMain
+    from test_node import _RefNodeStub
+    node = SudokuNode("127.0.0.1", 0, 0, engine=engine, delay_ms=0, api="main").start()
+    try:
+        code, body = _post(node.http_port, _grid(synth.WIKI))
+        assert code == 201 and list(body) == ["solution"]
+        assert "".join(str(v) for row in body["solution"] for v in row) == synth.WIKI_SOLUTION
+        code, net = _get(node.http_port, "/network")
+        assert set(net) == {"node", "predecessor", "neighbor"}
+    finally:
+        _stop([node])
+
+    class Node(HipSolveMixinMain, _RefNodeStub):
+        pass
+    for c in solve_cases:
+        nd = Node()
+        nd.sudoku_engine = engine
+        grid = [list(c["puzzle"][9 * r: 9 * r + 9]) for r in range(9)]
+        assert nd.solve_sudoku(grid, range(*c["range"])) == c["ok"], c["name"]
+        assert [v for row in grid for v in row] == (c["board"] if c["ok"] else c["puzzle"]), c["name"]

@@ -44,6 +44,7 @@ VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
 SOLVERS = {
     "halfwave": (1, "sdk::solve2_kernel", 8),
     "wave": (0, "sdk::solve_kernel", 3),
+    "quad": (2, "sdk::solve4_kernel", 8),
 }
 
 
@@ -60,8 +61,8 @@ def parse_args():
     ap.add_argument("--check-warmup", type=int, default=10,
                     help="untimed checker launches first (the memory clocks ramp under sustained streaming)")
     ap.add_argument("--order", choices=["mrv_unique", "lex"], default="mrv_unique")
-    ap.add_argument("--solver", choices=sorted(SOLVERS), default="halfwave",
-                    help="solve kernel: two boards per wave (solve2_kernel) or one (solve_kernel)")
+    ap.add_argument("--solver", choices=sorted(SOLVERS), default="quad",
+                    help="solve kernel: four boards per wave (solve4_kernel), two (solve2_kernel) or one (solve_kernel)")
     ap.add_argument("--waves-per-cu", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget per leg (0 = skip)")
     ap.add_argument("--cpu-cores", type=int, default=0,

@@ -1,0 +1,519 @@
+// solve4_kernel.h -- DHTNode.solve_sudoku (DHT_Node.py:474-538) on gfx950, FOUR
+// boards per wavefront: two per 32-lane half, packed as the two 16-bit halves of
+// every state word (SIMD within a register).
+//
+// Same search, rules and orders as solve2_kernel.h (and so the same answers and
+// the same search nodes per board); the lane layout is solve2's -- lane j < 27 of
+// a half owns cells j, j+27, j+54 and unit j -- but every 32-bit word carries the
+// same cell (or unit) of two boards: bits 0..15 board "lo", bits 16..31 board
+// "hi".  All propagation arithmetic is bitwise or packed 16-bit (v_pk_sub_u16,
+// v_pk_min_u16), so one instruction advances two boards and a propagation round
+// costs about half the VALU instructions per board of solve2's.
+//
+// Cell state, per board (16-bit field):
+//   X  bits 0..8: candidate digits 1..9;  bit 9: out-of-domain given (inert)
+//   S  the digit of a given or of a solved cell (one bit of 0..8), 0 if open;
+//      bit 9 for an inert given
+// so a cell is open (branchable) <=> S == 0; a given is X = S = its digit bit.
+// Givens are not otherwise marked: what solve2 reads from its "given" field is
+// static per board and kept per unit lane instead, computed once per board by a
+// static pass over the input (start of every board):
+//   D  digits given at least twice in the unit (given-vs-given duplicates: the
+//      reference never validates clues, SURVEY §0.9, so they are no conflict)
+//   E  0x1FF if the unit is exact (no duplicate and no inert given: every digit
+//      must occur exactly once in every completion), else 0
+// Unit summary (lane j, unit j, both boards): from the 9 cells (X, S) words
+//   T     = OR of S                      (taken digits: givens and solved cells)
+//   once  = X-digits held by exactly one cell, in exact units (hidden singles)
+//   conflict: a digit taken twice that is not a duplicated given, or an exact
+//             unit that lost a digit.  (A non-given cell can never be solved to
+//             a given digit of its units -- every rule only picks digits outside
+//             T -- so "taken twice, not in D" is solve2's solved-vs-solved /
+//             solved-vs-given test.  The first-cell `range` restriction is the
+//             exception: that cell starts OPEN with X = mask even when the mask
+//             is one digit, so round 1 eliminates T from it like any other cell.)
+// Cell update (open cells): X &= ~T;  hidden single X & once; two hidden singles
+// or no candidate = contradiction; one candidate left -> S = X (solved).
+//
+// Search per board: as solve2 (events = contradiction or fixpoint; count up to 2
+// completions under MRV, lex re-search when two are found; lowest-open-cell
+// branching under LEX).  A board's search step runs with its 16-bit field pulled
+// out of the packed words; the slot (lo/hi) is a compile-time constant of the step
+// (step4<0>, step4<1>), the two 32-lane halves take their steps under exec masks.
+// DFS snapshot per level: the three X fields of the lane (S is recomputed: at a
+// fixpoint, S = X exactly for the cells with one candidate).
+#pragma once
+#include "solve2_kernel.h"
+
+namespace sdk {
+
+#ifndef SDK_SOLVE4_LDS_LEVELS
+#define SDK_SOLVE4_LDS_LEVELS 2
+#endif
+#ifndef SDK_SOLVE4_WAVES_PER_EU
+#define SDK_SOLVE4_WAVES_PER_EU 6
+#endif
+// DFS levels kept in LDS (per level: 2 slots x 64 lanes x 8 B = 1 KiB; deeper levels go
+// to the per-workgroup global stack).  2 levels keep the block at 6.6 KiB, so 24 waves
+// (6 per SIMD at 80 VGPRs) fit a CU's 160 KiB.
+constexpr int kLds4Levels = SDK_SOLVE4_LDS_LEVELS;
+constexpr int kStack4WordsPerBlock = kMaxDepth * 2 * 64 * 2;
+constexpr uint32_t kC2 = 0x01FF01FFu;                 // candidate bits of both boards
+constexpr uint32_t kInert4 = 0x200u;                  // inert marker (one board)
+constexpr uint32_t kInert4x2 = 0x02000200u;
+
+// Packed 16-bit integer ops (every 16-bit half holds a value <= 0x3FF).  The masks
+// are inline asm: written as vector code, clang turns a sign mask and the select
+// it feeds into per-half compares, v_cndmask and v_perm, costing more than the
+// packing saves.  Inline constants apply to both halves (op_sel_hi:[0,1] for the
+// shift count).
+// per 16-bit half: 0xFFFF where the half is 0, else 0     ((a - 1) >>s 15)
+__device__ __forceinline__ uint32_t z16(uint32_t a) {
+    uint32_t r;
+    asm("v_pk_add_u16 %0, %1, -1\n\tv_pk_ashrrev_i16 %0, 15, %0 op_sel_hi:[0,1]" : "=&v"(r) : "v"(a));
+    return r;
+}
+// per 16-bit half: 0xFFFF where the half is not 0, else 0  ((0 - a) >>s 15)
+__device__ __forceinline__ uint32_t nz16(uint32_t a) {
+    uint32_t r;
+    asm("v_pk_sub_u16 %0, 0, %1\n\tv_pk_ashrrev_i16 %0, 15, %0 op_sel_hi:[0,1]" : "=&v"(r) : "v"(a));
+    return r;
+}
+// per 16-bit half: a - 1 (no borrow across the halves)
+__device__ __forceinline__ uint32_t dec16(uint32_t a) {
+    uint32_t r;
+    asm("v_pk_add_u16 %0, %1, -1" : "=v"(r) : "v"(a));
+    return r;
+}
+__device__ __forceinline__ uint32_t min16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+template <int HI>
+__device__ __forceinline__ uint32_t fld(uint32_t w) {
+    return HI ? (w >> 16) : (w & 0xFFFFu);
+}
+template <int HI>
+__device__ __forceinline__ uint32_t setfld(uint32_t w, uint32_t v) {
+    return HI ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
+}
+
+// Lane layout (solve2's).  Every lane, spare lanes 27..31 included, owns cells
+// c0, c0+27, c0+54 and reads the unit summaries ucol, ur0 + {0,3,6}, ub0 + {0,3,6},
+// so each group of three LDS accesses is one base register plus immediate offsets.
+// Spare lanes own the inert slots 81+e, 108+e, 135+e and read lane 0's units (their
+// cells are never open, so what they read does not matter; same addresses = broadcast).
+constexpr int kCells4 = 140;                          // LDS cell slots per half
+struct Lane4 {
+    int lane, hl, half;
+    bool act;
+    int c0;
+    int ucol, ur0, ub0;
+    int ucell[9];
+    uint2* s_cell;            // this half's kCells4 (X, S) words
+    uint2* s_unit;            // this half's 32 (T, once) words
+    uint8_t* s_in;            // this half's input bytes, [slot][81]
+};
+
+__device__ __forceinline__ void init_lane4(Lane4& w, uint2* s_cell_all, uint2* s_unit_all, uint8_t* s_in_all) {
+    Lane2 l2;
+    init_lane2(l2, nullptr, nullptr);
+    w.lane = l2.lane;
+    w.hl = l2.hl;
+    w.half = l2.half;
+    w.act = l2.act;
+    const int j = w.act ? w.hl : 0;
+    w.c0 = w.act ? j : 81 + (w.hl - 27);
+    w.ucol = 9 + j % 9;
+    w.ur0 = j / 9;
+    w.ub0 = 18 + (j % 9) / 3;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w.ucell[k] = l2.ucell[k];
+    w.s_cell = s_cell_all + w.half * kCells4;
+    w.s_unit = s_unit_all + w.half * 32;
+    w.s_in = s_in_all + w.half * 2 * 81;
+}
+
+__device__ __forceinline__ bool half_any4(const Lane4& w, bool pred) {
+    const unsigned long long b = __ballot(pred);
+    return (w.half ? (uint32_t)(b >> 32) : (uint32_t)b) != 0u;
+}
+
+__device__ __forceinline__ uint32_t half_first4(const Lane4& w, uint32_t v) {
+    return (uint32_t)__shfl((int)v, w.half * 32);
+}
+
+// a wave-uniform 64-bit lane mask with every 32-lane half that has a set bit filled
+__device__ __forceinline__ uint64_t spread_halves(uint64_t m) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)m) != 0u ? 0xFFFFFFFFu : 0u;
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) != 0u ? 0xFFFFFFFFu : 0u;
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// packed lane state: the lane's three cells of both boards of its half
+struct Cells4 {
+    uint32_t x0, x1, x2, s0, s1, s2;
+    uint32_t D, E;            // statics of the lane's unit (both boards)
+};
+
+// open-cell update of one cell of both boards (see the header)
+__device__ __forceinline__ void upd4(uint32_t& X, uint32_t& S, uint32_t U, uint32_t H, uint32_t& bm, uint32_t& zmin,
+                                     uint32_t& chg) {
+    const uint32_t v1 = X & ~U;
+    const uint32_t h = v1 & H;
+    const uint32_t hm = nz16(h);
+    const uint32_t v2 = (h & hm) | (v1 & ~hm);
+    bm |= h & dec16(h);                           // two hidden singles for one cell
+    const uint32_t om = z16(S);                   // open cells
+    const uint32_t xn = (v2 & om) | (X & ~om);
+    zmin = min16(zmin, xn | S);                   // an open cell without candidates
+    const uint32_t add = om & z16(v2 & dec16(v2)) & v2;   // open cell left with one candidate: solved
+    chg |= (xn ^ X) | add;
+    X = xn;
+    S |= add;
+}
+
+// One propagation round for all four boards, branch-free.  Out: per-lane packed
+// contradiction bits (bm, zmin) and change bits (chg).
+__device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, uint32_t& zmin, uint32_t& chg) {
+    w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
+    w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
+    w.s_cell[w.c0 + 54] = make_uint2(c.x2, c.s2);
+    __syncthreads();
+    uint32_t ox = 0, tx = 0, os = 0, ts = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const uint2 v = w.s_cell[w.ucell[k]];
+        tx |= ox & v.x;
+        ox |= v.x;
+        ts |= os & v.y;
+        os |= v.y;
+    }
+    bm = (ts & ~c.D & kC2) | (c.E & ~ox);
+    w.s_unit[w.hl] = make_uint2(os & kC2, ox & ~tx & c.E);
+    __syncthreads();
+    const uint2 uc = w.s_unit[w.ucol];
+    const uint2 r0 = w.s_unit[w.ur0], r1 = w.s_unit[w.ur0 + 3], r2 = w.s_unit[w.ur0 + 6];
+    const uint2 b0 = w.s_unit[w.ub0], b1 = w.s_unit[w.ub0 + 3], b2 = w.s_unit[w.ub0 + 6];
+    zmin = 0xFFFFFFFFu;
+    chg = 0;
+    upd4(c.x0, c.s0, uc.x | r0.x | b0.x, uc.y | r0.y | b0.y, bm, zmin, chg);
+    upd4(c.x1, c.s1, uc.x | r1.x | b1.x, uc.y | r1.y | b1.y, bm, zmin, chg);
+    upd4(c.x2, c.s2, uc.x | r2.x | b2.x, uc.y | r2.y | b2.y, bm, zmin, chg);
+}
+
+// per-slot search state, uniform within the half.  It lives in LDS between steps
+// (s_slot[half][slot]) and in registers only inside a step; the propagation loop
+// keeps just `active`.  Rounds are counted by the loop iteration (wave-uniform)
+// minus the iteration the board started at.
+struct Slot4 {
+    uint32_t bidx, bend;
+    uint32_t depth, order, count, lim;
+    uint32_t rstart, active;
+    uint64_t nodes;
+};
+
+__device__ __forceinline__ uint32_t cell_x4(uint32_t v) {
+    return v == 0 ? kCands : (v <= 9 ? (1u << (v - 1u)) : kInert4);
+}
+__device__ __forceinline__ uint32_t cell_s4(uint32_t v) {
+    return v == 0 ? 0u : (v <= 9 ? (1u << (v - 1u)) : kInert4);
+}
+// S of a cell restored from a snapshot: its X if one bit is set (given, solved, inert), else open
+__device__ __forceinline__ uint32_t s_of_x4(uint32_t x) {
+    return (x & (x - 1u)) == 0u ? x : 0u;
+}
+
+// kernel arguments as plain values plus the wave's propagation-loop iteration
+struct Args4 : Args2 {
+    uint32_t iter;
+};
+
+template <int HI>
+__device__ __forceinline__ void start_board4(const Lane4& w, const Args4& a, Slot4& b, Cells4& c, bool reload) {
+    uint32_t i0, i1, i2;
+    uint8_t* sin = w.s_in + HI * 81;
+    if (reload) {
+        const uint8_t* src = a.in + (a.in_first + (uint64_t)b.bidx * a.in_step) * 81;
+        i0 = w.act ? (uint32_t)src[w.c0] : 0u;
+        i1 = w.act ? (uint32_t)src[w.c0 + 27] : 0u;
+        i2 = w.act ? (uint32_t)src[w.c0 + 54] : 0u;
+        if (w.act) {
+            sin[w.c0] = (uint8_t)i0;
+            sin[w.c0 + 27] = (uint8_t)i1;
+            sin[w.c0 + 54] = (uint8_t)i2;
+        }
+    } else {
+        i0 = w.act ? (uint32_t)sin[w.c0] : 0u;
+        i1 = w.act ? (uint32_t)sin[w.c0 + 27] : 0u;
+        i2 = w.act ? (uint32_t)sin[w.c0 + 54] : 0u;
+    }
+    uint32_t x0 = w.act ? cell_x4(i0) : kInert4, x1 = w.act ? cell_x4(i1) : kInert4, x2 = w.act ? cell_x4(i2) : kInert4;
+    const uint32_t s0 = w.act ? cell_s4(i0) : kInert4, s1 = w.act ? cell_s4(i1) : kInert4,
+                   s2 = w.act ? cell_s4(i2) : kInert4;
+    if (a.mask) {
+        // TASK `range` restricts the lowest-index empty input cell only (DHT_Node.py:474,522,531);
+        // that cell starts open with X = mask, whatever the mask's size (see the header)
+        const uint32_t fm = ((uint32_t)a.mask[b.bidx] >> 1) & kCands;
+        uint32_t z = ~0u;
+        if (w.act)
+            z = i0 == 0 ? (uint32_t)w.c0 : (i1 == 0 ? (uint32_t)w.c0 + 27 : (i2 == 0 ? (uint32_t)w.c0 + 54 : ~0u));
+        z = half_min(z);
+        x0 = (w.act && z == (uint32_t)w.c0) ? fm : x0;
+        x1 = (w.act && z == (uint32_t)w.c0 + 27) ? fm : x1;
+        x2 = (w.act && z == (uint32_t)w.c0 + 54) ? fm : x2;
+    }
+    c.x0 = setfld<HI>(c.x0, x0);
+    c.x1 = setfld<HI>(c.x1, x1);
+    c.x2 = setfld<HI>(c.x2, x2);
+    c.s0 = setfld<HI>(c.s0, s0);
+    c.s1 = setfld<HI>(c.s1, s1);
+    c.s2 = setfld<HI>(c.s2, s2);
+    b.depth = 0;
+    b.count = 0;
+}
+
+// statics (D, E) of the lane's unit for the board in slot HI, from its input givens
+template <int HI>
+__device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
+    w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
+    w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
+    w.s_cell[w.c0 + 54] = make_uint2(c.x2, c.s2);
+    __syncthreads();
+    uint32_t os = 0, ts = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const uint32_t v = fld<HI>(w.s_cell[w.ucell[k]].y);
+        ts |= os & v;
+        os |= v;
+    }
+    __syncthreads();   // the next round's stores must not overtake these reads
+    const uint32_t dup = ts & kCands;
+    const uint32_t exact = (dup == 0u && (os & kInert4) == 0u) ? kCands : 0u;
+    c.D = setfld<HI>(c.D, dup);
+    c.E = setfld<HI>(c.E, exact);
+}
+
+template <int HI>
+__device__ __forceinline__ void next_board4(const Lane4& w, const Args4& a, Slot4& b, Cells4& c) {
+    ++b.bidx;
+    if (b.bidx >= b.bend) {
+        uint32_t base = 0;
+        if (w.hl == 0) base = atomicAdd(a.next, a.chunk);
+        base = half_first4(w, base);
+        b.bidx = base;
+        b.bend = (uint32_t)min((uint64_t)base + a.chunk, a.n);
+    }
+    b.active = (uint64_t)b.bidx < a.n ? 1u : 0u;
+    b.order = a.order == ORDER_LEX ? ORDER_LEX : ORDER_MRV;
+    b.lim = b.order == ORDER_LEX ? 1u : 2u;
+    b.nodes = 0;
+    b.rstart = a.iter;
+    if (b.active) {
+        start_board4<HI>(w, a, b, c, true);
+    } else {
+        c.x0 = setfld<HI>(c.x0, kInert4);
+        c.x1 = setfld<HI>(c.x1, kInert4);
+        c.x2 = setfld<HI>(c.x2, kInert4);
+        c.s0 = setfld<HI>(c.s0, kInert4);
+        c.s1 = setfld<HI>(c.s1, kInert4);
+        c.s2 = setfld<HI>(c.s2, kInert4);
+    }
+    statics4<HI>(w, c);
+}
+
+template <int HI>
+__device__ __forceinline__ void finish_board4(const Lane4& w, const Args4& a, Slot4& b, Cells4& c, int st) {
+    uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
+    if (st != 1 && w.act) {           // the reference restores the grid (DHT_Node.py:535)
+        const uint8_t* sin = w.s_in + HI * 81;
+        dst[w.c0] = sin[w.c0];
+        dst[w.c0 + 27] = sin[w.c0 + 27];
+        dst[w.c0 + 54] = sin[w.c0 + 54];
+    }
+    if (w.hl == 0) {
+        a.status[b.bidx] = (int8_t)st;
+        if (a.work) a.work[b.bidx] = a.work_rounds ? (uint64_t)(a.iter - b.rstart) : b.nodes;
+    }
+    next_board4<HI>(w, a, b, c);
+}
+
+__device__ __forceinline__ uint32_t branch_key4(uint32_t x, uint32_t s, int cell, int order) {
+    if (s != 0u) return ~0u;
+    const uint32_t base = ((uint32_t)cell << 9) | x;
+    return order == ORDER_LEX ? base : (((uint32_t)__popc(x)) << 16) | base;
+}
+
+// branch-free (selects): see solve2's set_cell2 on guarded updates of the three cells
+template <int HI>
+__device__ __forceinline__ void set_cell4(const Lane4& w, Cells4& c, int cell, uint32_t d) {
+    const bool k0 = w.act && cell == w.c0, k1 = w.act && cell == w.c0 + 27, k2 = w.act && cell == w.c0 + 54;
+    c.x0 = k0 ? setfld<HI>(c.x0, d) : c.x0;
+    c.s0 = k0 ? setfld<HI>(c.s0, d) : c.s0;
+    c.x1 = k1 ? setfld<HI>(c.x1, d) : c.x1;
+    c.s1 = k1 ? setfld<HI>(c.s1, d) : c.s1;
+    c.x2 = k2 ? setfld<HI>(c.x2, d) : c.x2;
+    c.s2 = k2 ? setfld<HI>(c.s2, d) : c.s2;
+}
+
+// the search step of the board in slot HI after its round ended (bad: contradiction)
+template <int HI>
+__device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4& b, Cells4& c, bool bad, uint32_t* s_br,
+                                           uint2 (*s_stk)[2][64], uint2* g_stk) {
+    ++b.nodes;
+    const uint32_t x0 = fld<HI>(c.x0), x1 = fld<HI>(c.x1), x2 = fld<HI>(c.x2);
+    const uint32_t s0 = fld<HI>(c.s0), s1 = fld<HI>(c.s1), s2 = fld<HI>(c.s2);
+    int r = bad ? P_CONTRA
+                : (half_any4(w, w.act && (s0 == 0u || s1 == 0u || s2 == 0u)) ? P_OPEN : P_SOLVED);
+    if (a.budget && b.nodes > a.budget) {
+        finish_board4<HI>(w, a, b, c, -2);
+        return;
+    }
+    if (r == P_SOLVED) {
+        ++b.count;
+        if (b.count == 1 && w.act) {
+            uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
+            const uint8_t* sin = w.s_in + HI * 81;
+            const uint32_t i0 = sin[w.c0], i1 = sin[w.c0 + 27], i2 = sin[w.c0 + 54];
+            dst[w.c0] = (uint8_t)(i0 == 0 ? (uint32_t)__ffs(x0) : i0);
+            dst[w.c0 + 27] = (uint8_t)(i1 == 0 ? (uint32_t)__ffs(x1) : i1);
+            dst[w.c0 + 54] = (uint8_t)(i2 == 0 ? (uint32_t)__ffs(x2) : i2);
+        }
+        if (b.count >= b.lim) {
+            if (b.order == ORDER_MRV) {      // >= 2 completions: lex re-search
+                b.order = ORDER_LEX;
+                b.lim = 1;
+                start_board4<HI>(w, a, b, c, false);
+            } else {
+                finish_board4<HI>(w, a, b, c, 1);
+            }
+            return;
+        }
+        r = P_CONTRA;
+    }
+    uint32_t* br = s_br + (w.half * 2 + HI) * kMaxDepth;
+    if (r == P_OPEN) {
+        uint32_t key = ~0u;
+        if (w.act)
+            key = min(branch_key4(x0, s0, w.c0, b.order),
+                      min(branch_key4(x1, s1, w.c0 + 27, b.order), branch_key4(x2, s2, w.c0 + 54, b.order)));
+        key = half_min(key);
+        const int cell = (int)((key >> 9) & 0x7Fu);
+        const uint32_t m = key & kCands;
+        const uint32_t d = m & (0u - m);
+        const uint2 snap = make_uint2(x0 | (x1 << 16), x2);
+        if (b.depth < kLds4Levels) s_stk[b.depth][HI][w.lane] = snap;
+        else g_stk[(b.depth * 2 + HI) * 64 + w.lane] = snap;
+        if (w.hl == 0) br[b.depth] = (uint32_t)cell | ((m ^ d) << 16);
+        ++b.depth;
+        set_cell4<HI>(w, c, cell, d);
+        return;
+    }
+    // contradiction: resume the deepest level with untried digits
+    if (b.depth == 0) {
+        finish_board4<HI>(w, a, b, c, b.count > 0 ? 1 : 0);
+        return;
+    }
+    const uint32_t rec = br[b.depth - 1];
+    const int cell = (int)(rec & 0xFFu);
+    uint32_t rest = rec >> 16;
+    const uint32_t d = rest & (0u - rest);
+    rest ^= d;
+    const uint2 snap =
+        b.depth - 1 < kLds4Levels ? s_stk[b.depth - 1][HI][w.lane] : g_stk[((b.depth - 1) * 2 + HI) * 64 + w.lane];
+    const uint32_t y0 = snap.x & 0xFFFFu, y1 = snap.x >> 16, y2 = snap.y;
+    c.x0 = setfld<HI>(c.x0, y0);
+    c.x1 = setfld<HI>(c.x1, y1);
+    c.x2 = setfld<HI>(c.x2, y2);
+    c.s0 = setfld<HI>(c.s0, s_of_x4(y0));
+    c.s1 = setfld<HI>(c.s1, s_of_x4(y1));
+    c.s2 = setfld<HI>(c.s2, s_of_x4(y2));
+    if (rest == 0) --b.depth;
+    else if (w.hl == 0) br[b.depth - 1] = (uint32_t)cell | (rest << 16);
+    set_cell4<HI>(w, c, cell, d);
+}
+
+// step of slot HI: its state comes from and returns to LDS; returns whether the slot is active
+template <int HI>
+__device__ __forceinline__ bool step4(const Lane4& w, const Args4& a, Cells4& c, bool bad, uint32_t* s_br,
+                                      uint2 (*s_stk)[2][64], uint2* g_stk, Slot4* s_slot) {
+    Slot4* p = s_slot + w.half * 2 + HI;
+    Slot4 b = *p;
+    step4_body<HI>(w, a, b, c, bad, s_br, s_stk, g_stk);
+    if (w.hl == 0) *p = b;
+    return b.active != 0u;
+}
+
+// first board of slot HI (all lanes)
+template <int HI>
+__device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cells4& c, Slot4* s_slot) {
+    Slot4 b;
+    b.bidx = 0xFFFFFFFFu;   // ++ -> 0 >= bend = 0: first dequeue
+    b.bend = 0;
+    b.depth = 0;
+    b.count = 0;
+    next_board4<HI>(w, a, b, c);
+    if (w.hl == 0) s_slot[w.half * 2 + HI] = b;
+    return b.active != 0u;
+}
+
+#ifdef SDK_DEFINE_SOLVE4_KERNEL   // defined in solve4_launch.hip only
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {
+    __shared__ uint2 s_cell[2 * kCells4];
+    __shared__ uint2 s_unit[2 * 32];
+    __shared__ uint8_t s_in[2 * 2 * 81];
+    __shared__ uint32_t s_br[2 * 2 * kMaxDepth];
+    __shared__ uint2 s_stk[kLds4Levels][2][64];
+    __shared__ Slot4 s_slot[4];
+    Lane4 w;
+    init_lane4(w, s_cell, s_unit, s_in);
+    uint2* g_stk = reinterpret_cast<uint2*>(args.stack) + (size_t)blockIdx.x * (kMaxDepth * 2 * 64);
+    Args4 a;
+    a.in = args.in;
+    a.in_first = args.in_first;
+    a.in_step = args.in_step;
+    a.mask = args.mask;
+    a.next = args.next;
+    a.chunk = args.chunk;
+    a.n = args.n;
+    a.order = args.order;
+    a.out = args.out;
+    a.status = args.status;
+    a.work = args.work;
+    a.work_rounds = args.work_rounds;
+    a.budget = args.budget;
+    a.iter = 0;
+
+    Cells4 c;
+    c.x0 = c.x1 = c.x2 = c.s0 = c.s1 = c.s2 = kInert4x2;
+    c.D = 0;
+    c.E = 0;
+    bool act0 = first_board4<0>(w, a, c, s_slot);
+    bool act1 = first_board4<1>(w, a, c, s_slot);
+
+    // Event detection in scalar registers: one ballot per (flag, slot), each spread
+    // to the 32 lanes of the half it came from; a slot's board takes its search step
+    // when it contradicted (B) or nothing changed (no C) in its half.
+    for (;;) {
+        const uint64_t A0 = __builtin_amdgcn_ballot_w64(act0), A1 = __builtin_amdgcn_ballot_w64(act1);
+        if ((A0 | A1) == 0) break;
+        uint32_t bm, zmin, chg;
+        round4(w, c, bm, zmin, chg);
+        ++a.iter;
+        const uint32_t badw = bm | z16(zmin);
+        const uint64_t B0 = spread_halves(__builtin_amdgcn_ballot_w64((badw & 0xFFFFu) != 0u));
+        const uint64_t B1 = spread_halves(__builtin_amdgcn_ballot_w64(badw > 0xFFFFu));
+        const uint64_t C0 = spread_halves(__builtin_amdgcn_ballot_w64((chg & 0xFFFFu) != 0u));
+        const uint64_t C1 = spread_halves(__builtin_amdgcn_ballot_w64(chg > 0xFFFFu));
+        const uint64_t E0 = A0 & (B0 | ~C0), E1 = A1 & (B1 | ~C1);
+        if (E0 != 0 && __builtin_amdgcn_inverse_ballot_w64(E0))
+            act0 = step4<0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_br, s_stk, g_stk, s_slot);
+        if (E1 != 0 && __builtin_amdgcn_inverse_ballot_w64(E1))
+            act1 = step4<1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_br, s_stk, g_stk, s_slot);
+    }
+}
+#endif  // SDK_DEFINE_SOLVE4_KERNEL
+
+}  // namespace sdk

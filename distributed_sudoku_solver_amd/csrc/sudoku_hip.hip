@@ -20,9 +20,11 @@
 #include "solve_kernel.h"
 #include "frontier_kernel.h"
 #include "solve2_kernel.h"   // constants only: the kernel lives in solve2_launch.hip
+#include "solve4_kernel.h"   // constants only: the kernel lives in solve4_launch.hip
 
 namespace sdk {
 hipError_t launch_solve2(const SolveArgs& a, unsigned grid, hipStream_t stream);
+hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream);
 }
 
 namespace {
@@ -69,8 +71,8 @@ struct sdk_ctx {
     int check_variant = SDK_CHECK_REG1;
     int solve_chunk = 0;          // boards per dequeue, 0 = automatic
     int work_rounds = 0;
-    int solver = SDK_SOLVER_HALFWAVE;
-    int waves_per_cu2 = 32;       // solve2_kernel grid per CU (24 resident: 80 VGPRs, 6.8 KB LDS; the rest
+    int solver = SDK_SOLVER_QUAD;
+    int waves_per_cu2 = 32;       // solve2/solve4 grid per CU (24 resident: 80 VGPRs, <= 6.8 KB LDS; the rest
                                   // start as the first retire, and the smaller dequeue chunk trims the tail)
     // workspaces
     DevBuf stack, counter, in, mask, out, status, work, verdict;
@@ -153,10 +155,12 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
                  int order = -1) {
     if (n == 0) return SDK_OK;
     if (n > 0x7FFFFFFFull) return fail(SDK_EINVAL, "at most 2^31-1 boards per call");
-    // two boards per wave (solve2_kernel) for solves; count mode stays one board per wave
-    const bool two = !count_mode && c->solver == SDK_SOLVER_HALFWAVE;
-    if (two && (!d_out || !d_status)) return fail(SDK_EINVAL, "solve needs out and status buffers");
-    const uint64_t slots = (uint64_t)c->cus * (two ? c->waves_per_cu2 : c->waves_per_cu) * (two ? 2 : 1);
+    // two (solve2_kernel) or four (solve4_kernel) boards per wave for solves; count mode stays
+    // one board per wave
+    const int per_wave = count_mode ? 1 : (c->solver == SDK_SOLVER_QUAD ? 4 : (c->solver == SDK_SOLVER_HALFWAVE ? 2 : 1));
+    const bool two = per_wave == 2, four = per_wave == 4;
+    if ((two || four) && (!d_out || !d_status)) return fail(SDK_EINVAL, "solve needs out and status buffers");
+    const uint64_t slots = (uint64_t)c->cus * (per_wave > 1 ? c->waves_per_cu2 : c->waves_per_cu) * per_wave;
     // 16 boards per dequeue (fewer when a slot would get < 2 dequeues).  All dequeues hit ONE
     // counter and same-address atomics serialise at ~10 ns each: below ~16 boards the cheap
     // C2 boards (1.15 ns per board chip-wide) become dequeue-bound; above it the C4 tail grows
@@ -166,9 +170,9 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
         : c->solve_chunk ? (uint32_t)c->solve_chunk
         : (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, n / (slots * 2)));
     const uint64_t want = (n + chunk - 1) / chunk;
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(two ? (want + 1) / 2 : want,
-                                                                             two ? slots / 2 : slots));
-    const size_t stack_words = two ? sdk::kStack2WordsPerBlock : sdk::kStackWordsPerBlock;
+    const unsigned grid = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>((want + per_wave - 1) / per_wave, slots / per_wave));
+    const size_t stack_words = four ? sdk::kStack4WordsPerBlock : (two ? sdk::kStack2WordsPerBlock : sdk::kStackWordsPerBlock);
     int rc = ensure(c->stack, (size_t)grid * stack_words * sizeof(uint32_t));
     if (rc) return rc;
     rc = ensure(c->counter, 256);
@@ -196,7 +200,9 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
     if (rc) return rc;
-    if (two) {
+    if (four) {
+        HIPCALL(sdk::launch_solve4(a, grid, c->stream));
+    } else if (two) {
         HIPCALL(sdk::launch_solve2(a, grid, c->stream));
     } else {
         sdk::solve_kernel<<<grid, 64, 0, c->stream>>>(a);
@@ -450,7 +456,8 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             c->timing = value != 0;
             return SDK_OK;
         case SDK_OPT_SOLVER:
-            if (value != SDK_SOLVER_WAVE && value != SDK_SOLVER_HALFWAVE) return fail(SDK_EINVAL, "bad solver %lld", (long long)value);
+            if (value != SDK_SOLVER_WAVE && value != SDK_SOLVER_HALFWAVE && value != SDK_SOLVER_QUAD)
+                return fail(SDK_EINVAL, "bad solver %lld", (long long)value);
             c->solver = (int)value;
             return SDK_OK;
         case SDK_OPT_WAVES_PER_CU2:

@@ -68,8 +68,8 @@ extern "C" {
 #define SDK_OPT_CHECK_BLOCKS_PER_CU 4 /* checker grid = CUs x this, 1..16 (default 3)  */
 #define SDK_OPT_WORK_COUNTER 5  /* what solve `work` counts: SDK_WORK_* (default nodes) */
 #define SDK_OPT_DEVICE_CUS   6  /* read-only: compute units of the context's GPU        */
-#define SDK_OPT_SOLVER       7  /* solve kernel: SDK_SOLVER_* (default HALFWAVE)         */
-#define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE solver per CU, 1..32 (default 32) */
+#define SDK_OPT_SOLVER       7  /* solve kernel: SDK_SOLVER_* (default QUAD)             */
+#define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE / QUAD solver per CU, 1..32 (default 32) */
 #define SDK_OPT_CHECK_VARIANT 9 /* checker tile pipeline: SDK_CHECK_* (default REG1) */
 #define SDK_OPT_SOLVE_CHUNK  10  /* boards per solver dequeue, 0 = automatic (default)  */
 #define SDK_OPT_TIMING       11  /* 1 = bracket every kernel with HIP events for        */
@@ -84,6 +84,8 @@ extern "C" {
 
 #define SDK_SOLVER_WAVE      0  /* one board per wavefront (solve_kernel)              */
 #define SDK_SOLVER_HALFWAVE  1  /* two boards per wavefront, 27 lanes x 3 cells each   */
+#define SDK_SOLVER_QUAD      2  /* four boards per wavefront: HALFWAVE's layout with two */
+                                /* boards packed in the 16-bit halves of every word      */
 
 #define SDK_WORK_NODES       0  /* search nodes (propagation fixpoints)                */
 #define SDK_WORK_ROUNDS      1  /* propagation rounds (profiling)                      */

@@ -11,25 +11,26 @@ pytestmark = pytest.mark.gpu
 ORDERS = [L.SDK_ORDER_MRV_UNIQUE, L.SDK_ORDER_LEX]
 
 
-SOLVERS = [L.SDK_SOLVER_HALFWAVE, L.SDK_SOLVER_WAVE]
+SOLVERS = [L.SDK_SOLVER_HALFWAVE, L.SDK_SOLVER_WAVE, L.SDK_SOLVER_QUAD]
+SOLVER_IDS = ["halfwave", "wave", "quad"]
 
 
 @pytest.fixture(params=[(s, o) for s in SOLVERS for o in ORDERS],
-                ids=["halfwave-mrv_unique", "halfwave-lex", "wave-mrv_unique", "wave-lex"])
+                ids=[f"{n}-{o}" for n in SOLVER_IDS for o in ("mrv_unique", "lex")])
 def ordered_engine(request, engine):
     solver, order = request.param
     engine.set_option(L.SDK_OPT_SOLVER, solver)
     engine.set_option(L.SDK_OPT_ORDER, order)
     yield engine
     engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
-    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE)
+    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
 
 
-@pytest.fixture(params=SOLVERS, ids=["halfwave", "wave"])
+@pytest.fixture(params=SOLVERS, ids=SOLVER_IDS)
 def solver_engine(request, engine):
     engine.set_option(L.SDK_OPT_SOLVER, request.param)
     yield engine
-    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE)
+    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
 
 
 def test_golden_solve_cases(ordered_engine, solve_cases):
@@ -320,16 +321,19 @@ def test_solvers_take_identical_search_paths(engine):
             engine.set_option(L.SDK_OPT_WORK_COUNTER, kind)
             res[(solver, kind)] = engine.solve_batch(boards, want_work=True)
     engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
-    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE)
+    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
     for kind in (L.SDK_WORK_NODES, L.SDK_WORK_ROUNDS):
-        a, b = res[(SOLVERS[0], kind)], res[(SOLVERS[1], kind)]
-        assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
-        assert (a[2] == b[2]).all(), kind
+        a = res[(SOLVERS[0], kind)]
+        for other in SOLVERS[1:]:
+            b = res[(other, kind)]
+            assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
+            assert (a[2] == b[2]).all(), (kind, other)
 
 
 @pytest.mark.parametrize("chunk", [1, 7, 100, 4096])
-def test_dequeue_chunk_override(engine, chunk):
+def test_dequeue_chunk_override(solver_engine, chunk):
     """Any boards-per-dequeue gives the same boards (chunks straddling the batch end included)."""
+    engine = solver_engine
     p, s = synth.make_17clue(20_011, seed=77)
     try:
         engine.set_option(L.SDK_OPT_SOLVE_CHUNK, chunk)

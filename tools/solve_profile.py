@@ -18,15 +18,16 @@ ap.add_argument("--workload", default="solve17")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--stats", action="store_true")
 ap.add_argument("--waves-per-cu", type=int, default=0)
-ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave"])
+ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave", "quad"])
 ap.add_argument("--sweep", action="store_true", help="time waves-per-CU settings")
 args = ap.parse_args()
 
 gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
 p, s = gen(args.n, seed=11)
 with SudokuEngine(0) as eng:
-    eng.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_HALFWAVE if args.solver == "halfwave" else L.SDK_SOLVER_WAVE)
-    wopt = L.SDK_OPT_WAVES_PER_CU2 if args.solver == "halfwave" else L.SDK_OPT_WAVES_PER_CU
+    eng.set_option(L.SDK_OPT_SOLVER, {"halfwave": L.SDK_SOLVER_HALFWAVE, "wave": L.SDK_SOLVER_WAVE,
+                                      "quad": L.SDK_SOLVER_QUAD}[args.solver])
+    wopt = L.SDK_OPT_WAVES_PER_CU if args.solver == "wave" else L.SDK_OPT_WAVES_PER_CU2
     if args.waves_per_cu:
         eng.set_option(wopt, args.waves_per_cu)
     d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)

@@ -124,6 +124,7 @@ class SudokuNode:
         self.neighbor_tasks = []                 # tasks handed to the neighbour (re-run on its failure)
         self.busy = False
         self.done_uuids = set()                  # uuids already solved somewhere in the ring
+        self.best = {}                           # uuid -> (lowest digit, grid): best ordered completion so far
         self.waiters = {}                        # uuid -> (Event, [solution], puzzle, failed digit mask)
         self.trace = collections.deque(maxlen=4096) if trace else None   # (method, addr, range) sent
         self.validations = 0
@@ -141,6 +142,8 @@ class SudokuNode:
         self.http_port = self.httpd.server_address[1]
         self._threads = []
         self._work = threading.Condition()
+        self._go = threading.Event()             # cleared by pause(): the worker holds its queue
+        self._go.set()
 
     # ------------------------------------------------------------------ utils
     def _log(self, *a):
@@ -258,9 +261,13 @@ class SudokuNode:
             for node in net:
                 if node != self.me:
                     self.send({"method": "UPDATE_NETWORK", "network": net, "coordinator": self.coordinator}, node)
-            # joiner is appended last: it follows net[-2] and precedes net[0]
-            self.send({"method": "UPDATE_PREDECESSOR", "predecessor": joiner}, net[0])
-            self.send({"method": "UPDATE_NEIGHBOR", "neighbor": joiner}, net[-2])
+            # joiner is appended last: it follows net[-2] and precedes net[0]; updates meant
+            # for this node are applied below, not sent to itself (a late self-datagram
+            # would reset neighborfree after the joiner's NEEDWORK arrived)
+            if net[0] != self.me:
+                self.send({"method": "UPDATE_PREDECESSOR", "predecessor": joiner}, net[0])
+            if net[-2] != self.me:
+                self.send({"method": "UPDATE_NEIGHBOR", "neighbor": joiner}, net[-2])
             self.send({"method": "JOIN_RES", "predecessor": net[-2], "neighbor": net[0], "network": net,
                        "coordinator": self.coordinator}, joiner)
             if net[0] == self.me:
@@ -302,13 +309,9 @@ class SudokuNode:
             self.coordinator = _addr(msg["coordinator"])
 
     def _on_SOLUTION_FOUND(self, msg):
-        uid = msg.get("uuid")
         with self.lock:
             self.solved_count += 1
-            if uid is not None:
-                self.done_uuids.add(uid)
-                self._purge(uid)
-        self._wake(uid, msg.get("solution"))
+        self._solution(msg.get("uuid"), msg.get("solution"), msg.get("range"))
 
     def _on_NO_SOLUTION(self, msg):
         self._failed(msg.get("uuid"), msg.get("range"), msg.get("sudoku"))
@@ -387,16 +390,21 @@ class SudokuNode:
             except queue.Empty:
                 return out
 
-    def _purge(self, uid):
-        keep = [t for t in self._drain_queue() if t.get("uuid") != uid]
+    def _purge(self, uid, above=None):
+        """Drop the tasks of puzzle `uid` (only those whose lowest digit is above `above`, if given)."""
+        def drop(t):
+            return t.get("uuid") == uid and (above is None or _lowest_digit(t.get("range")) > above)
+        keep = [t for t in self._drain_queue() if not drop(t)]
         for t in keep:
             self.tasks.put(t)
-        self.neighbor_tasks = [t for t in self.neighbor_tasks if t.get("uuid") != uid]
+        self.neighbor_tasks = [t for t in self.neighbor_tasks if not drop(t)]
 
     def _maybe_delegate(self):
-        """A free neighbour gets one queued task (DHT_Node.py:491-498)."""
+        """A free neighbour gets one queued task (DHT_Node.py:491-498) -- only while this node
+        is busy (the reference hands work over from inside solve_sudoku); an idle node's
+        worker takes its queue itself."""
         with self.lock:
-            if not (self.neighborfree and self.neighbor and self.neighbor != self.me):
+            if not (self.busy and self.neighborfree and self.neighbor and self.neighbor != self.me):
                 return
             try:
                 t = self.tasks.get_nowait()
@@ -406,10 +414,19 @@ class SudokuNode:
             self.neighbor_tasks.append(t)
             self.send(t, self.neighbor)
 
+    def pause(self):
+        """Hold the worker: TASKs queue up (and are batched together on resume())."""
+        self._go.clear()
+
+    def resume(self):
+        self._go.set()
+        with self._work:
+            self._work.notify()
+
     def _worker_loop(self):
         while self.running:
             with self._work:
-                while self.running and self.tasks.empty():
+                while self.running and (self.tasks.empty() or not self._go.is_set()):
                     self._work.wait(0.5)
             if not self.running:
                 return
@@ -474,7 +491,7 @@ class SudokuNode:
                     for c in range(9):
                         if grid[r][c] == 0:
                             grid[r][c] = int(o[9 * r + c])
-                self._solved(uid, grid, t.get("initial_node"))
+                self._solved(t, grid)
             else:
                 if st == L.SDK_BUDGET_HIT:
                     self._log("budget exhausted for", uid)
@@ -487,25 +504,73 @@ class SudokuNode:
                     self.send({"method": "NO_SOLUTION", "uuid": uid, "range": t.get("range", range(1, 10)),
                                "sudoku": t["sudoku"], "node": self.me}, origin)
 
-    def _solved(self, uid, grid, origin=None):
+    def _solved(self, task, grid):
+        """This node completed `task`: SOLUTION_FOUND to every peer (and the HTTP origin).  A
+        task that came from an HTTP origin (it carries `initial_node`) also reports its digit
+        range, so the origin can keep the reference's single-node answer (see _solution)."""
+        uid = task.get("uuid")
+        origin = _addr(task.get("initial_node"))
+        arr = task.get("range", range(1, 10)) if origin is not None else None
         with self.lock:
-            if uid is not None:              # main.py TASKs carry no uuid (main.py:359-360)
-                if uid in self.done_uuids:
-                    return
-                self.done_uuids.add(uid)
-                self._purge(uid)
-            self.solved_count += 1
+            if uid is not None and uid in self.done_uuids:
+                return
+            self.solved_count += 1                       # perform_solving, DHT_Node.py:428
             peers = [n for n in self.network if n != self.me]
-        origin = _addr(origin)
         if origin is not None and origin != self.me and origin not in peers:
             peers.append(origin)
+        msg = {"method": "SOLUTION_FOUND", "solution": grid, "node": self.me, "uuid": uid}
+        if arr is not None:
+            msg["range"] = arr
         for node in peers:
-            self.send({"method": "SOLUTION_FOUND", "solution": grid, "node": self.me, "uuid": uid}, node)
-        self._wake(uid, grid)
+            self.send(msg, node)
+        self._solution(uid, grid, arr)
+
+    def _solution(self, uid, grid, arr):
+        """A completion of puzzle `uid` was found with its first empty cell in digit range `arr`.
+
+        arr None (a reference node's report, or a split of a partial board): final, as in the
+        reference (DHT_Node.py:348-387).  Otherwise ranges of one puzzle are ordered: tasks
+        whose digits all lie above `arr` are dropped, lower ones keep running, and the HTTP
+        origin answers with the lowest-range completion once every lower digit has failed --
+        the lexicographically first completion, whichever node finishes first."""
+        if uid is None:                              # main.py TASKs carry no uuid (main.py:359-360)
+            return
+        lo = _lowest_digit(arr) if arr is not None else None
+        with self.lock:
+            if uid in self.done_uuids:
+                return
+            if lo is None:
+                self.done_uuids.add(uid)
+                self._purge(uid)
+                self.best.pop(uid, None)
+                final = grid
+            else:
+                best = self.best.get(uid)
+                if best is None or lo < best[0]:
+                    self.best[uid] = (lo, grid)
+                self._purge(uid, above=lo)
+                final = self._accept(uid)
+        if final is not None:
+            self._wake(uid, final)
+
+    def _accept(self, uid):
+        """(under self.lock) The origin's best completion if every digit below its range failed."""
+        w = self.waiters.get(uid)
+        best = self.best.get(uid)
+        if w is None or best is None:
+            return None
+        need = ((1 << best[0]) - 1) & ALL_DIGITS_MASK          # digits 1 .. lo-1
+        if (w[3][0] & need) != need:
+            return None
+        self.done_uuids.add(uid)
+        self._purge(uid)
+        del self.best[uid]
+        return best[1]
 
     def _failed(self, uid, arr, sudoku):
-        """A range of puzzle `uid` has no completion: wake its HTTP waiter once every digit of
-        the first empty cell has failed (only reports about the waiter's own board count)."""
+        """A range of puzzle `uid` has no completion: the HTTP origin answers once the failed
+        ranges cover every digit of the first empty cell (only reports about its own board
+        count), or accepts a waiting upper-range completion once everything below it failed."""
         try:
             m = range_to_mask(arr if arr is not None else range(1, 10))
             board = encode_solve_grid(sudoku)
@@ -516,8 +581,13 @@ class SudokuNode:
             if w is None or not np.array_equal(w[2], board):
                 return
             w[3][0] |= m
-            done = (w[3][0] & ALL_DIGITS_MASK) == ALL_DIGITS_MASK
-        if done:
+            final = self._accept(uid)
+            none_left = final is None and (w[3][0] & ALL_DIGITS_MASK) == ALL_DIGITS_MASK
+            if none_left:
+                self.done_uuids.add(uid)
+        if final is not None:
+            self._wake(uid, final)
+        elif none_left:
             self._wake(uid, None)
 
     def _wake(self, uid, solution, error=None):
@@ -540,6 +610,7 @@ class SudokuNode:
         ok = ev.wait(self.solve_timeout_s)
         with self.lock:
             self.waiters.pop(uid, None)
+            self.best.pop(uid, None)
         if not ok:
             raise TimeoutError("no solution reported in time")
         res = box[0] if box else None
@@ -585,6 +656,15 @@ class SudokuNode:
             net = list(self.network)
         n = len(net)
         return {str(a): [str(net[(i - 1) % n]), str(net[(i + 1) % n])] for i, a in enumerate(net)}
+
+
+def _lowest_digit(arr):
+    """Lowest digit 1..9 of a TASK range (10 if none)."""
+    try:
+        m = range_to_mask(arr if arr is not None else range(1, 10))
+    except (TypeError, ValueError):
+        return 1
+    return (m & -m).bit_length() - 1 if m else 10
 
 
 class _Failure:

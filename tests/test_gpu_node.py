@@ -67,8 +67,7 @@ def test_concurrent_posts_batch_into_few_launches(engine):
     try:
         p, s = S.make_17clue(64, seed=123)
         res = [None] * 64
-        with node.lock:
-            node.busy = True               # hold the worker until every request is queued
+        node.pause()                       # hold the worker until every request is queued
         ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, _post(node.http_port, _grid("".join(map(str, p[i]))))))
                for i in range(64)]
         for t in ths:
@@ -76,10 +75,7 @@ def test_concurrent_posts_batch_into_few_launches(engine):
         t0 = time.time()
         while node.tasks.qsize() < 64 and time.time() - t0 < 30:
             time.sleep(0.01)
-        with node.lock:
-            node.busy = False
-        with node._work:
-            node._work.notify()
+        node.resume()
         for t in ths:
             t.join(60)
         for i in range(64):

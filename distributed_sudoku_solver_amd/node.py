@@ -136,7 +136,7 @@ class SudokuNode:
         self.sock.settimeout(0.2)
         self.port = self.sock.getsockname()[1]
         self.me = (host, self.port)
-        self.httpd = ThreadingHTTPServer((host, http_port), _Handler)
+        self.httpd = _Server((host, http_port), _Handler)
         self.httpd.node = self
         self.httpd.daemon_threads = True
         self.http_port = self.httpd.server_address[1]
@@ -676,6 +676,12 @@ def _validate_task(msg):
     """Raise unless a TASK can be launched: a 9x9 (or flat 81) grid and an ascending 0..9 range."""
     encode_solve_grid(msg["sudoku"])
     range_to_mask(msg.get("range", range(1, 10)))
+
+
+class _Server(ThreadingHTTPServer):
+    # bursts of concurrent POST /solve are what the batched launch is for: the
+    # socketserver default listen backlog of 5 would drop their connections
+    request_queue_size = 256
 
 
 class _Handler(BaseHTTPRequestHandler):

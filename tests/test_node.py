@@ -412,3 +412,29 @@ def test_lex_first_even_when_upper_half_finishes_first():
         assert any(t[0] == "SOLUTION_FOUND" and t[1] == a.me and t[2] == range(5, 10) for t in b.trace), _diag(a, b)
     finally:
         _stop([a, b])
+
+
+def test_http_burst_is_one_launch():
+    """64 concurrent POST /solve (listen backlog > socketserver's 5) drain into one launch."""
+    import threading
+    node = SudokuNode("127.0.0.1", 0, 0, engine=OracleEngine(), delay_ms=0).start()
+    try:
+        p, s = synth.make_30clue(64, seed=123)
+        res = [None] * 64
+        node.pause()
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, _post(node.http_port, _grid("".join(map(str, p[i]))))))
+               for i in range(64)]
+        for t in ths:
+            t.start()
+        t0 = time.time()
+        while node.tasks.qsize() < 64 and time.time() - t0 < 30:
+            time.sleep(0.01)
+        node.resume()
+        for t in ths:
+            t.join(60)
+        assert all(r is not None and r[0] == 201 for r in res)
+        assert ["".join(str(v) for row in r[1]["solution"] for v in row) for r in res] == \
+            ["".join(map(str, x)) for x in s]
+        assert node.engine.batches == [64]
+    finally:
+        _stop([node])

@@ -74,6 +74,8 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=20250614)
     ap.add_argument("--c2-puzzles", type=int, default=1_000_000,
                     help="C2 leg: ~30-clue unique puzzles per GPU (0 = skip)")
+    ap.add_argument("--minimal-puzzles", type=int, default=65536,
+                    help="distinct minimal-puzzle leg, puzzles per GPU (0 = skip)")
     ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
                     help="watchdog for the side legs: print what was measured and exit")
@@ -298,6 +300,26 @@ def c5_rebalanced_leg(eng, d, synth):
             "ok": total == C5_14CLUE_SOLUTIONS and st == 1, "frontier_boards": size,
             "rounds": info.get("rounds"), "steals": info.get("steals"),
             "wall_ms": w * 1000.0, "value": total / w, "unit": "solutions/s"}
+
+
+def minimal_leg(eng, d, args, synth, L):
+    """Robustness leg beside C4: DISTINCT minimal unique puzzles (random grids, clues removed while
+    the completion stays unique, 21-29 clues; csrc/gen_minimal.c), resident in HBM, checked against
+    their generating grids, with the search-tail statistics (nodes, max DFS depth) of the same set."""
+    n = args.minimal_puzzles
+    p, s = synth.make_minimal(n, lo=d.rank * n, threads=cpu_share())
+    el, k_s, bad = solve_leg(eng, d, args, p, s, 3, 1)
+    stats = {}
+    for kind, name in ((L.SDK_WORK_NODES, "nodes"), (L.SDK_WORK_ROUNDS, "rounds"), (L.SDK_WORK_DEPTH, "depth")):
+        eng.set_option(L.SDK_OPT_WORK_COUNTER, kind)
+        _, _, w = eng.solve_batch(p, want_work=True)
+        stats[name] = {"mean": float(w.mean()), "p50": float(np.percentile(w, 50)),
+                       "p99": float(np.percentile(w, 99)), "max": int(w.max())}
+    eng.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
+    return {"workload": f"{n} distinct minimal unique puzzles per GPU (random grids, {int((p > 0).sum(1).mean())} "
+                        "clues on average)",
+            "value": d.world * n * 3 / el, "unit": "puzzles/s", "avg_kernel_ms": k_s * 1000.0,
+            "search": stats, "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
 
 
 def http_leg(requests):
@@ -553,6 +575,11 @@ def main():
     # ------------------------------------------------------------ C2 leg
     if args.c2_puzzles > 0:
         result["c2_30clue"] = c2_leg(eng, d, args, synth)
+
+    # ------------------------------------------------ distinct minimal puzzles
+    if args.minimal_puzzles > 0:
+        result["minimal_puzzles"] = minimal_leg(eng, d, args, synth, L)
+        bad_total += result["minimal_puzzles"]["parity"]["mismatched_boards"]
 
     # ------------------------------------------------------------ C5 leg
     if args.count_leg:

@@ -48,6 +48,7 @@ SDK_SOLVER_QUAD = 2
 
 SDK_WORK_NODES = 0
 SDK_WORK_ROUNDS = 1
+SDK_WORK_DEPTH = 2
 
 SDK_ORDER_MRV_UNIQUE = 0
 SDK_ORDER_LEX = 1

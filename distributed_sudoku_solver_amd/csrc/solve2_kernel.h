@@ -240,6 +240,7 @@ struct Board2 {
     int depth, order;
     uint32_t count, lim;
     uint64_t nodes, rounds;
+    uint32_t maxd;                // deepest DFS level reached (SDK_WORK_DEPTH)
     uint32_t in0, in1, in2;       // input bytes of the lane's cells
     uint32_t s0, s1, s2;          // cell states
 };
@@ -305,6 +306,7 @@ __device__ __forceinline__ void next_board(const Lane2& w, const Args2& a, Board
     b.order = a.order == ORDER_LEX ? ORDER_LEX : ORDER_MRV;
     b.lim = b.order == ORDER_LEX ? 1u : 2u;
     b.nodes = b.rounds = 0;
+    b.maxd = 0;
     if (b.active) start_board(w, a, b, true);
     else b.s0 = b.s1 = b.s2 = kInert2;
 }
@@ -318,7 +320,7 @@ __device__ __forceinline__ void finish_board(const Lane2& w, const Args2& a, Boa
     }
     if (w.hl == 0) {
         a.status[b.bidx] = (int8_t)st;
-        if (a.work) a.work[b.bidx] = a.work_rounds ? b.rounds : b.nodes;
+        if (a.work) a.work[b.bidx] = a.work_rounds == 1 ? b.rounds : (a.work_rounds == 2 ? (uint64_t)b.maxd : b.nodes);
     }
     next_board(w, a, b);
 }
@@ -405,6 +407,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void so
             else g_stk[b.depth * 64 + w.lane] = snap;
             if (w.hl == 0) s_br[w.half][b.depth] = (uint32_t)cell | ((m ^ d) << 16);
             ++b.depth;
+            b.maxd = max(b.maxd, (uint32_t)b.depth);
             set_cell2(w, b.s0, b.s1, b.s2, cell, d);
             continue;
         }

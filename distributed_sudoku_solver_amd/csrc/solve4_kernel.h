@@ -212,6 +212,7 @@ struct Slot4 {
     uint32_t bidx, bend;
     uint32_t depth, order, count, lim;
     uint32_t rstart, active;
+    uint32_t maxd;            // deepest DFS level reached (SDK_WORK_DEPTH)
     uint64_t nodes;
 };
 
@@ -310,6 +311,7 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Args4& a, Slot
     b.order = a.order == ORDER_LEX ? ORDER_LEX : ORDER_MRV;
     b.lim = b.order == ORDER_LEX ? 1u : 2u;
     b.nodes = 0;
+    b.maxd = 0;
     b.rstart = a.iter;
     if (b.active) {
         start_board4<HI>(w, a, b, c, true);
@@ -335,7 +337,9 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Args4& a, Sl
     }
     if (w.hl == 0) {
         a.status[b.bidx] = (int8_t)st;
-        if (a.work) a.work[b.bidx] = a.work_rounds ? (uint64_t)(a.iter - b.rstart) : b.nodes;
+        if (a.work)
+            a.work[b.bidx] = a.work_rounds == 1 ? (uint64_t)(a.iter - b.rstart)
+                                                : (a.work_rounds == 2 ? (uint64_t)b.maxd : b.nodes);
     }
     next_board4<HI>(w, a, b, c);
 }
@@ -408,6 +412,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
         else g_stk[(b.depth * 2 + HI) * 64 + w.lane] = snap;
         if (w.hl == 0) br[b.depth] = (uint32_t)cell | ((m ^ d) << 16);
         ++b.depth;
+        b.maxd = max(b.maxd, b.depth);
         set_cell4<HI>(w, c, cell, d);
         return;
     }

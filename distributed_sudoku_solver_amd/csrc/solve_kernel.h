@@ -73,7 +73,7 @@ struct SolveArgs {
     unsigned long long* counts;// count mode: per-board counts (nullable)
     int count_mode;
     uint32_t chunk;            // boards per dequeue (one atomic on `next` per chunk)
-    int work_rounds;           // work[] counts propagation rounds instead of search nodes
+    int work_rounds;           // what work[] counts: 0 search nodes, 1 propagation rounds, 2 max DFS depth
     uint64_t in_first;         // board i of the launch reads in[(in_first + i*in_step)*81];
     uint64_t in_step;          // outputs stay dense (out[i*81], status[i]); 0/1 = contiguous
 };
@@ -199,8 +199,8 @@ __device__ __forceinline__ void set_cell(const Wave& w, uint32_t& sa, uint32_t& 
 // or -1 when the node budget ran out.  The first completion is written to
 // `sol` when non-null.
 __device__ __forceinline__ int64_t search(const Wave& w, int order, uint32_t sa0, uint32_t sb0, uint64_t limit,
-                          uint64_t budget, uint64_t& nodes, uint64_t& rounds, uint8_t* sol, uint32_t inA,
-                          uint32_t inB) {
+                          uint64_t budget, uint64_t& nodes, uint64_t& rounds, uint64_t& maxd, uint8_t* sol,
+                          uint32_t inA, uint32_t inB) {
     uint32_t sa = sa0, sb = sb0;
     int depth = 0;
     int64_t count = 0;
@@ -239,6 +239,7 @@ __device__ __forceinline__ int64_t search(const Wave& w, int order, uint32_t sa0
             w.stk[depth * 64 + w.lane] = sa | (sb << 16);
             if (w.lane == 0) w.s_br[depth] = (uint32_t)cell | ((m ^ d) << 16);
             ++depth;
+            maxd = max(maxd, (uint64_t)depth);
             set_cell(w, sa, sb, cell, d);
             continue;
         }
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(64, 8) void solve_kernel(SolveArgs a) {
                 if (lane == (int)__builtin_ctzll(zb)) sb &= fm | ~kCands;
             }
             uint8_t* dst = a.out ? a.out + i * 81 : nullptr;
-            uint64_t nodes = 0, rounds = 0;
+            uint64_t nodes = 0, rounds = 0, maxd = 0;
             int8_t st;
             // count mode: whole-subtree count (order-independent, so MRV); the
             // batch stops early once the running total reaches the limit.
@@ -337,9 +338,9 @@ __global__ __launch_bounds__(64, 8) void solve_kernel(SolveArgs a) {
             const int order0 = (a.count_mode || a.order != ORDER_LEX) ? ORDER_MRV : ORDER_LEX;
             const uint64_t lim0 = a.count_mode ? a.limit : (order0 == ORDER_LEX ? 1u : 2u);
             int64_t c = 0;
-            if (!skip) c = search(w, order0, sa, sb, lim0, a.budget, nodes, rounds, dst, inA, inB);
+            if (!skip) c = search(w, order0, sa, sb, lim0, a.budget, nodes, rounds, maxd, dst, inA, inB);
             if (!a.count_mode && order0 == ORDER_MRV && c >= 2)
-                c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, rounds, dst, inA, inB);
+                c = search(w, ORDER_LEX, sa, sb, 1, a.budget, nodes, rounds, maxd, dst, inA, inB);
             if (a.count_mode && lane == 0) {
                 if (c > 0) atomicAdd(a.count, (unsigned long long)c);
                 if (a.counts) a.counts[i] = (unsigned long long)(c < 0 ? 0 : c);
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(64, 8) void solve_kernel(SolveArgs a) {
             if (dst && c <= 0) write_board(w, dst, inA, inB, sa, sb, false);
             if (lane == 0) {
                 if (a.status) a.status[i] = st;
-                if (a.work) a.work[i] = a.work_rounds ? rounds : nodes;
+                if (a.work) a.work[i] = a.work_rounds == 1 ? rounds : (a.work_rounds == 2 ? maxd : nodes);
             }
         }
     }

@@ -444,7 +444,8 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             c->check_blocks_per_cu = (int)value;
             return SDK_OK;
         case SDK_OPT_WORK_COUNTER:
-            if (value != SDK_WORK_NODES && value != SDK_WORK_ROUNDS) return fail(SDK_EINVAL, "bad work counter %lld", (long long)value);
+            if (value != SDK_WORK_NODES && value != SDK_WORK_ROUNDS && value != SDK_WORK_DEPTH)
+                return fail(SDK_EINVAL, "bad work counter %lld", (long long)value);
             c->work_rounds = (int)value;
             return SDK_OK;
         case SDK_OPT_DEVICE_CUS:

@@ -89,6 +89,7 @@ extern "C" {
 
 #define SDK_WORK_NODES       0  /* search nodes (propagation fixpoints)                */
 #define SDK_WORK_ROUNDS      1  /* propagation rounds (profiling)                      */
+#define SDK_WORK_DEPTH       2  /* deepest DFS level reached (profiling, tests)         */
 
 #define SDK_ORDER_MRV_UNIQUE 0  /* MRV search for <=2 solutions; lex re-search if >=2 */
 #define SDK_ORDER_LEX        1  /* lowest-index branching after propagation            */

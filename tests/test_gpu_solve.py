@@ -386,3 +386,34 @@ def test_timing_is_opt_in():
         assert eng.timer_read()[1] == 1
     finally:
         eng.close()
+
+
+def test_minimal_unique_puzzles_100k(engine):
+    """100k DISTINCT minimal unique puzzles (random grids, clues removed while unique; not the
+    S1-S5 isomorphism classes): every board equals its generating grid, a budgeted sample equals
+    the oracle's naive DFS (the reference's answer), and the deep-DFS path (global stack beyond
+    the LDS-resident levels) is exercised: depth > 10 under LEX."""
+    p, s = synth.make_minimal(100_000, threads=16)
+    assert len({bytes(x) for x in p}) == len(p)
+    out, st, nodes = engine.solve_batch(p, want_work=True)
+    assert (st == 1).all() and (out == s).all()
+    ref_out, ref_st, _ = O.naive_solve_batch(p[:2000], budget=20_000_000, threads=16)
+    done = ref_st == 1
+    assert done.mean() > 0.9 and (out[:2000][done] == ref_out[done]).all()
+    sparse = _random_puzzles(2000, 91, 8, 20)             # multi-solution: LEX goes deep
+    boards = np.concatenate([p[:20000], sparse, np.zeros((1, 81), np.uint8)])
+    ref_out2, ref_st2, _ = O.naive_solve_batch(boards[20000:], budget=20_000_000, threads=16)
+    try:
+        engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_DEPTH)
+        for solver in SOLVERS:
+            engine.set_option(L.SDK_OPT_SOLVER, solver)
+            engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
+            o2, st2, depth = engine.solve_batch(boards, want_work=True)
+            assert (o2[:20000] == s[:20000]).all() and (st2[:20000] == 1).all()
+            ok = ref_st2 != -2
+            assert (o2[20000:][ok] == ref_out2[ok]).all() and (st2[20000:][ok] == ref_st2[ok]).all()
+            assert depth.max() > 10, (solver, int(depth.max()))
+    finally:
+        engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
+        engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+        engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)

@@ -293,7 +293,17 @@ def c5_rebalanced_leg(eng, d, synth):
         if comm is not None:
             comm.close()
     w = min(walls)
-    return {"workload": "C5: count every completion of a 14-clue board (S1, last row cleared, one more clue "
+    # frontier scale: a ~1M-board frontier of the same board (tile scan over the chip,
+    # device-side level loop), timed alone
+    fw = []
+    for _ in range(3):
+        eng.synchronize()
+        t0 = time.perf_counter()
+        fsize, _ = eng.frontier_build(board, target=1_000_000)
+        fw.append(time.perf_counter() - t0)
+    info["frontier_1m"] = {"boards": fsize, "build_ms": 1000 * min(fw)}
+    return {"frontier_1m": info.get("frontier_1m"),
+            "workload": "C5: count every completion of a 14-clue board (S1, last row cleared, one more clue "
                         f"removed), rebalanced frontier over {d.world} GPU(s)"
                         + (", RCCL all-gather of live ranges + all-reduce" if d.world > 1 else ""),
             "solutions": total, "expected": C5_14CLUE_SOLUTIONS,

@@ -10,11 +10,16 @@
 //                  propagated board is written back with every single-valued
 //                  cell as a given (a fixpoint has no conflict among them, so
 //                  treating them as givens changes no completion).
-//   scan_kernel    exclusive prefix sum of nchild (one 1024-thread workgroup,
-//                  wave-level __shfl_up scans + LDS for the wave totals).
+//   scan_tiles_kernel + scan_top_kernel   exclusive prefix sum of nchild over
+//                  the whole chip: every workgroup scans 4096-entry tiles
+//                  (wave __shfl_up scans + LDS for the wave totals) and writes
+//                  the tile total; one workgroup then scans the tile totals.
 //   emit_kernel    one wave per parent writes its children contiguously at
-//                  offset[parent], digits ascending: children of one parent
-//                  and parents in order -> a coalesced, ordered HBM array.
+//                  offset[parent] + tile offset, digits ascending: children of
+//                  one parent and parents in order -> a coalesced, ordered HBM array.
+// The level loop runs on the device: every kernel reads the frontier size and a
+// stop flag from FrontierCtl (frontier_begin/end_kernel update them), so the host
+// enqueues levels without waiting and reads the control block every few levels.
 //   first_hit_kernel  after a batched solve of frontier boards [lo, hi): the
 //                  lowest index whose status is not "no solution" and its board.
 //
@@ -30,16 +35,27 @@
 
 namespace sdk {
 
+// device-side control block of one frontier build
+struct FrontierCtl {
+    unsigned long long m;        // boards in the current frontier
+    unsigned long long leaves;   // completions met while expanding (count mode), cumulative
+    unsigned long long open;     // boards that branched in the current level
+    unsigned long long total;    // children of the current level (scan)
+    unsigned int level;          // completed levels: the frontier is in buffer (level & 1)
+    unsigned int done;           // 1 = expansion finished
+    unsigned int next;           // expand_kernel dequeue counter
+    unsigned int pad;
+};
+
+constexpr int kScanTile = 4096;   // entries per scan tile (1024 threads x 4)
+
 struct ExpandArgs {
     const uint8_t* in;
-    uint64_t m;
+    FrontierCtl* ctl;
     uint8_t* prop;            // [m][81] propagated board (singles as givens)
     uint8_t* bcell;           // [m] branch cell
     uint16_t* bmask;          // [m] branch candidates (bit d-1 = digit d)
     uint32_t* nchild;         // [m]
-    unsigned long long* leaves;
-    unsigned long long* open;  // boards that branched at this level
-    uint32_t* next;
     int order;
     const uint16_t* mask;      // nullable, level 0 only: first-cell digit mask of board 0
     int keep_leaves;           // first-solution mode (see header)
@@ -54,19 +70,42 @@ __device__ __forceinline__ uint32_t board_byte(uint32_t in, uint32_t s) {
     return is_single(v) ? (uint32_t)__ffs(v) : 0u;
 }
 
+// level start: stop when the frontier is empty or reached `target` (level 0 with a
+// first-cell mask always runs: the mask lives only in that level's expansion)
+__global__ void frontier_begin_kernel(FrontierCtl* ctl, uint64_t target, int force) {
+    if (ctl->done) return;
+    if (ctl->m == 0 || (ctl->m >= target && !force) || ctl->level >= 81) {
+        ctl->done = 1;
+        return;
+    }
+    ctl->next = 0;
+    ctl->open = 0;
+}
+
+// level end: the children become the frontier; first-solution mode stops when nothing
+// branched (the next level would equal this one)
+__global__ void frontier_end_kernel(FrontierCtl* ctl, int first) {
+    if (ctl->done) return;
+    ctl->m = ctl->total;
+    ctl->level += 1;
+    if (ctl->total == 0 || (first && ctl->open == 0)) ctl->done = 1;
+}
+
 __global__ __launch_bounds__(64) void expand_kernel(ExpandArgs a) {
     __shared__ uint32_t s_cell[96];
     __shared__ uint32_t s_unit[32];
     __shared__ uint32_t s_br[4];
+    if (a.ctl->done) return;
+    const uint64_t m_lvl = a.ctl->m;
     Wave w;
     init_wave(w, s_cell, s_unit, s_br);
     const int lane = w.lane;
     for (;;) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.next, kChunk);
+        if (lane == 0) base = atomicAdd(&a.ctl->next, kChunk);
         base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-        if ((uint64_t)base >= a.m) break;
-        const uint64_t end = min((uint64_t)base + kChunk, a.m);
+        if ((uint64_t)base >= m_lvl) break;
+        const uint64_t end = min((uint64_t)base + kChunk, m_lvl);
         for (uint64_t i = base; i < end; ++i) {
             const uint8_t* src = a.in + i * 81;
             const uint32_t inA = src[lane];
@@ -95,10 +134,10 @@ __global__ __launch_bounds__(64) void expand_kernel(ExpandArgs a) {
                     dst[lane] = (uint8_t)board_byte(inA, sa);
                     if (w.hasB) dst[64 + lane] = (uint8_t)board_byte(inB, sb);
                 } else if (lane == 0) {
-                    atomicAdd(a.leaves, 1ull);
+                    atomicAdd(&a.ctl->leaves, 1ull);
                 }
             } else if (r == P_OPEN) {
-                if (lane == 0) atomicAdd(a.open, 1ull);
+                if (lane == 0) atomicAdd(&a.ctl->open, 1ull);
                 const uint32_t pa = open_count(sa);
                 const uint32_t pb = w.hasB ? open_count(sb) : 0u;
                 unsigned long long ma, mb;
@@ -131,17 +170,61 @@ __global__ __launch_bounds__(64) void expand_kernel(ExpandArgs a) {
     }
 }
 
-// Exclusive scan of n uint32 counts into uint64 offsets; total written to *total.
-__global__ __launch_bounds__(1024) void scan_kernel(const uint32_t* __restrict__ cnt, uint64_t* __restrict__ off,
-                                                     uint64_t n, unsigned long long* total) {
+// Tile-local exclusive scan: tile t = entries [t*4096, (t+1)*4096) of nchild[0..m);
+// off[i] = prefix within the tile, tsum[t] = tile total.  Grid-stride over tiles.
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(const uint32_t* __restrict__ cnt, uint64_t* __restrict__ off,
+                                                          const FrontierCtl* ctl, uint64_t* __restrict__ tsum) {
+    __shared__ uint32_t s_wave[16];
+    if (ctl->done) return;
+    const uint64_t n = ctl->m;
+    const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        const uint64_t i0 = tile * kScanTile + 4u * (uint64_t)t;
+        uint32_t x[4], own = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            x[k] = i0 + k < n ? cnt[i0 + k] : 0u;
+            own += x[k];
+        }
+        uint32_t inc = own;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, d);
+            if (lane >= d) inc += y;
+        }
+        if (lane == 63) s_wave[wv] = inc;
+        __syncthreads();
+        uint32_t wbase = 0, all = 0;
+        for (int k = 0; k < 16; ++k) {
+            wbase += k < wv ? s_wave[k] : 0u;
+            all += s_wave[k];
+        }
+        uint32_t run = wbase + inc - own;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (i0 + k < n) off[i0 + k] = run;
+            run += x[k];
+        }
+        if (t == 0) tsum[tile] = all;
+        __syncthreads();
+    }
+}
+
+// Exclusive scan of the tile totals in place (one workgroup); the level's child count
+// goes to ctl->total, and a level whose children exceed `cap` boards stops the build
+// (the frontier stays the current one).
+__global__ __launch_bounds__(1024) void scan_top_kernel(uint64_t* __restrict__ tsum, FrontierCtl* ctl, uint64_t cap) {
     __shared__ uint64_t s_wave[16];
     __shared__ uint64_t s_carry;
+    if (ctl->done) return;
+    const uint64_t n = (ctl->m + kScanTile - 1) / kScanTile;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (t == 0) s_carry = 0;
     __syncthreads();
     for (uint64_t base = 0; base < n; base += 1024) {
         const uint64_t i = base + t;
-        const uint64_t x = i < n ? cnt[i] : 0;
+        const uint64_t x = i < n ? tsum[i] : 0;
         uint64_t inc = x;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -153,17 +236,23 @@ __global__ __launch_bounds__(1024) void scan_kernel(const uint32_t* __restrict__
         uint64_t wbase = 0;
         for (int k = 0; k < wv; ++k) wbase += s_wave[k];
         const uint64_t carry = s_carry;
-        if (i < n) off[i] = carry + wbase + inc - x;
+        if (i < n) tsum[i] = carry + wbase + inc - x;
         __syncthreads();
         if (t == 1023) s_carry = carry + wbase + inc;
         __syncthreads();
     }
-    if (t == 0) *total = s_carry;
+    if (t == 0) {
+        ctl->total = s_carry;
+        if (s_carry > cap) ctl->done = 1;
+    }
 }
 
 __global__ __launch_bounds__(64) void emit_kernel(const uint8_t* __restrict__ prop, const uint8_t* __restrict__ bcell,
                                                   const uint16_t* __restrict__ bmask, const uint64_t* __restrict__ off,
-                                                  uint64_t m, uint8_t* __restrict__ out) {
+                                                  const uint64_t* __restrict__ tsum, const FrontierCtl* ctl,
+                                                  uint8_t* __restrict__ out) {
+    if (ctl->done) return;
+    const uint64_t m = ctl->m;
     const int lane = threadIdx.x;
     const bool hasB = lane < 17;
     for (uint64_t i = blockIdx.x; i < m; i += gridDim.x) {
@@ -171,7 +260,7 @@ __global__ __launch_bounds__(64) void emit_kernel(const uint8_t* __restrict__ pr
         if (!mask) continue;
         const uint32_t a = prop[i * 81 + lane];
         const uint32_t b = hasB ? prop[i * 81 + 64 + lane] : 0u;
-        uint64_t j = off[i];
+        uint64_t j = off[i] + tsum[i / kScanTile];
         if (mask & kKeepBoard) {   // solved leaf kept in place (first-solution mode)
             uint8_t* dst = out + j * 81;
             dst[lane] = (uint8_t)a;

@@ -76,10 +76,11 @@ struct sdk_ctx {
                                   // start as the first retire, and the smaller dequeue chunk trims the tail)
     // workspaces
     DevBuf stack, counter, in, mask, out, status, work, verdict;
-    DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask;
+    DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
     // the device-resident frontier of the last sdk_frontier_build (in fr_a)
     uint64_t fr_size = 0;
     uint64_t fr_leaves = 0;
+    uint32_t fr_levels = 0;
     bool fr_valid = false;
     // RCCL communicator (sdk_comm_init), one rank per context
     ncclComm_t comm = nullptr;
@@ -222,72 +223,70 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
 int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, int mode, uint64_t target) {
     int rc;
     c->fr_valid = false;
-    // counters: [0] next (u32), [1] level leaves (u64), [2] scan total, [3] count total, [4] level open
-    if ((rc = ensure(c->counter, 256)) || (rc = ensure(c->fr_a, 81)) || (rc = ensure(c->fr_mask, 16))) return rc;
-    unsigned long long* ctr = static_cast<unsigned long long*>(c->counter.p);
-    HIPCALL(hipMemcpyAsync(c->fr_a.p, h_board, 81, hipMemcpyHostToDevice, c->stream));
-    if (h_mask) HIPCALL(hipMemcpyAsync(c->fr_mask.p, h_mask, 2, hipMemcpyHostToDevice, c->stream));
     if (target == 0) target = (uint64_t)c->cus * (uint64_t)c->waves_per_cu * 8ull;
     const uint64_t cap = 1ull << 25;  // 32M boards (2.6 GB) per frontier buffer
     const bool first = mode == SDK_FRONTIER_FIRST;
-    uint64_t m = 1, leaves = 0;
-    int level = 0;
-    // a first-cell mask lives only in level 0's expansion: that level always runs
-    while (m > 0 && (m < target || (level == 0 && h_mask)) && level < 81) {
-        if ((rc = ensure(c->prop, m * 81)) || (rc = ensure(c->bcell, m)) || (rc = ensure(c->bmask, m * 2)) ||
-            (rc = ensure(c->nchild, m * 4)) || (rc = ensure(c->offs, m * 8)))
-            return rc;
-        HIPCALL(hipMemsetAsync(c->counter.p, 0, 40, c->stream));
+    // Buffers are sized once for the whole build, so the levels can be enqueued without
+    // the host: a level is expanded only while the frontier is below `target` (or at
+    // level 0), and a level with more than `cap` children is rejected.
+    const uint64_t m_exp = std::max<uint64_t>(1, std::min(target, cap));
+    const uint64_t c_out = std::max<uint64_t>(1, std::min(cap, 9 * m_exp));
+    const uint64_t tiles = (m_exp + sdk::kScanTile - 1) / sdk::kScanTile;
+    if ((rc = ensure(c->fr_a, c_out * 81)) || (rc = ensure(c->fr_b, c_out * 81)) || (rc = ensure(c->fr_mask, 16)) ||
+        (rc = ensure(c->prop, m_exp * 81)) || (rc = ensure(c->bcell, m_exp)) || (rc = ensure(c->bmask, m_exp * 2)) ||
+        (rc = ensure(c->nchild, m_exp * 4)) || (rc = ensure(c->offs, m_exp * 8)) || (rc = ensure(c->tsum, tiles * 8)) ||
+        (rc = ensure(c->fr_ctl, sizeof(sdk::FrontierCtl))))
+        return rc;
+    sdk::FrontierCtl* ctl = static_cast<sdk::FrontierCtl*>(c->fr_ctl.p);
+    sdk::FrontierCtl h{};
+    h.m = 1;
+    HIPCALL(hipMemcpyAsync(ctl, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+    HIPCALL(hipMemcpyAsync(c->fr_a.p, h_board, 81, hipMemcpyHostToDevice, c->stream));
+    if (h_mask) HIPCALL(hipMemcpyAsync(c->fr_mask.p, h_mask, 2, hipMemcpyHostToDevice, c->stream));
+    void* buf[2] = {c->fr_a.p, c->fr_b.p};
+    const unsigned eg = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>((m_exp + sdk::kChunk - 1) / sdk::kChunk, (uint64_t)c->cus * c->waves_per_cu));
+    const unsigned sg = (unsigned)std::min<uint64_t>(tiles, (uint64_t)c->cus * 4);
+    const unsigned gg = (unsigned)std::min<uint64_t>(m_exp, (uint64_t)c->cus * 32);
+    hipEvent_t stop;
+    if ((rc = timer_begin(c, &stop))) return rc;
+    constexpr int kLevelsPerSync = 4;
+    for (int level = 0; level < 81; ++level) {
+        const int in = level & 1;
+        sdk::frontier_begin_kernel<<<1, 1, 0, c->stream>>>(ctl, target, level == 0 && h_mask ? 1 : 0);
         sdk::ExpandArgs ea;
-        ea.in = static_cast<const uint8_t*>(c->fr_a.p);
-        ea.m = m;
+        ea.in = static_cast<const uint8_t*>(buf[in]);
+        ea.ctl = ctl;
         ea.prop = static_cast<uint8_t*>(c->prop.p);
         ea.bcell = static_cast<uint8_t*>(c->bcell.p);
         ea.bmask = static_cast<uint16_t*>(c->bmask.p);
         ea.nchild = static_cast<uint32_t*>(c->nchild.p);
-        ea.leaves = ctr + 1;
-        ea.open = ctr + 4;
-        ea.next = static_cast<uint32_t*>(c->counter.p);
         ea.order = first ? sdk::ORDER_LEX : sdk::ORDER_MRV;
         ea.mask = (level == 0 && h_mask) ? static_cast<const uint16_t*>(c->fr_mask.p) : nullptr;
         ea.keep_leaves = first ? 1 : 0;
-        const unsigned eg = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m + sdk::kChunk - 1) / sdk::kChunk,
-                                                                               (uint64_t)c->cus * c->waves_per_cu));
-        hipEvent_t stop;
-        if ((rc = timer_begin(c, &stop))) return rc;
         sdk::expand_kernel<<<eg, 64, 0, c->stream>>>(ea);
+        sdk::scan_tiles_kernel<<<sg, 1024, 0, c->stream>>>(static_cast<uint32_t*>(c->nchild.p),
+                                                           static_cast<uint64_t*>(c->offs.p), ctl,
+                                                           static_cast<uint64_t*>(c->tsum.p));
+        sdk::scan_top_kernel<<<1, 1024, 0, c->stream>>>(static_cast<uint64_t*>(c->tsum.p), ctl, c_out);
+        sdk::emit_kernel<<<gg, 64, 0, c->stream>>>(static_cast<uint8_t*>(c->prop.p), static_cast<uint8_t*>(c->bcell.p),
+                                                   static_cast<uint16_t*>(c->bmask.p), static_cast<uint64_t*>(c->offs.p),
+                                                   static_cast<uint64_t*>(c->tsum.p), ctl,
+                                                   static_cast<uint8_t*>(buf[in ^ 1]));
+        sdk::frontier_end_kernel<<<1, 1, 0, c->stream>>>(ctl, first ? 1 : 0);
         HIPCALL(hipGetLastError());
-        sdk::scan_kernel<<<1, 1024, 0, c->stream>>>(static_cast<uint32_t*>(c->nchild.p),
-                                                    static_cast<uint64_t*>(c->offs.p), m, ctr + 2);
-        HIPCALL(hipGetLastError());
-        unsigned long long h[5] = {0, 0, 0, 0, 0};
-        HIPCALL(hipMemcpyAsync(h, c->counter.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
-        HIPCALL(hipStreamSynchronize(c->stream));
-        const uint64_t total = h[2], lvl_leaves = h[1], open = h[4];
-        // level rejected: its children would not fit; fr_a stays as it is
-        if (total > cap) {
-            if ((rc = timer_end(c, stop))) return rc;
-            break;
+        if (level % kLevelsPerSync == kLevelsPerSync - 1 || level == 80) {
+            HIPCALL(hipMemcpyAsync(&h, ctl, sizeof h, hipMemcpyDeviceToHost, c->stream));
+            HIPCALL(hipStreamSynchronize(c->stream));
+            if (h.done) break;
         }
-        if (total && (rc = ensure(c->fr_b, total * 81))) return rc;
-        if (total) {
-            const unsigned gg = (unsigned)std::min<uint64_t>(m, (uint64_t)c->cus * 32);
-            sdk::emit_kernel<<<gg, 64, 0, c->stream>>>(static_cast<uint8_t*>(c->prop.p), static_cast<uint8_t*>(c->bcell.p),
-                                                       static_cast<uint16_t*>(c->bmask.p),
-                                                       static_cast<uint64_t*>(c->offs.p), m,
-                                                       static_cast<uint8_t*>(c->fr_b.p));
-            HIPCALL(hipGetLastError());
-        }
-        if ((rc = timer_end(c, stop))) return rc;
-        std::swap(c->fr_a, c->fr_b);
-        m = total;
-        leaves += lvl_leaves;
-        ++level;
-        if (first && open == 0) break;   // nothing branched: the next level would equal this one
     }
+    if ((rc = timer_end(c, stop))) return rc;
     HIPCALL(hipStreamSynchronize(c->stream));
-    c->fr_size = m;
-    c->fr_leaves = leaves;
+    if (h.level & 1) std::swap(c->fr_a, c->fr_b);   // the final frontier lives in fr_a
+    c->fr_size = h.m;
+    c->fr_leaves = h.leaves;
+    c->fr_levels = h.level;
     c->fr_valid = true;
     return SDK_OK;
 }
@@ -412,7 +411,7 @@ int sdk_destroy(sdk_ctx* c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (DevBuf* b : {&c->stack, &c->counter, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
                       &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status,
-                      &c->fr_mask})
+                      &c->fr_mask, &c->tsum, &c->fr_ctl})
         if (b->p) (void)hipFree(b->p);
     for (auto& pr : c->events) {
         (void)hipEventDestroy(pr.first);

@@ -417,3 +417,26 @@ def test_minimal_unique_puzzles_100k(engine):
         engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
         engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
         engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
+
+
+def test_frontier_1m_boards_multiworkgroup_scan(engine):
+    """A ~1M-board frontier (tile scan across the chip, device-side level loop) still counts
+    every completion of the 14-clue board, and its slices partition the count."""
+    s1 = synth.SEEDS17["S1"]
+    b14 = synth.parse(s1[:-18] + "000100000" + "0" * 9)
+    size, leaves = engine.frontier_build(b14, mode=L.SDK_FRONTIER_COUNT, target=1_000_000)
+    assert size >= 1_000_000
+    res = engine.result_buffer(2, np.uint64)
+    total = leaves
+    for r in range(3):
+        engine.frontier_count(r, 3, size, 0, res)
+        cnt, hits = engine.read(res, 2, np.uint64)
+        assert hits == 0
+        total += int(cnt)
+    res.free()
+    assert total == 18_204_270
+    # first-solution mode at a large target: the reference's answer for the demo board
+    from distributed_sudoku_solver_amd.shard import sharded_solve
+    out, st = sharded_solve(engine, synth.parse(DEMO), 0, 1, target=300_000)
+    assert st == 1 and "".join(map(str, out)) == \
+        "234156789179328456568479132391245678425687391687913245752831964816794523943562817"

@@ -76,6 +76,7 @@ SIGNATURES = {
     "sdk_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int64]),
     "sdk_get_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
     "sdk_check_batch": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
+    "sdk_check_batch_i64": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
     "sdk_solve_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz]),
     "sdk_count_solutions": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.POINTER(ctypes.c_int8)]),

@@ -278,4 +278,52 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel_glds(const uint8_t
     wait_vmcnt<0>();
 }
 
+// ---------------------------------------------------------------------------
+// check_kernel_i64 -- the same literal rule on int64 cells, for boards whose values
+// leave 0..255 (the reference takes any Python int; JSON numbers reach it unchanged).
+// One thread per board; not bandwidth-tuned (an off-nominal input path).  Valid for
+// |v| < 2^59, where the sum of 9 cells cannot overflow (the host checks the bound).
+__device__ __forceinline__ bool unit_ok_i64(const int64_t (&u)[9]) {
+    int64_t sum = 0;
+    bool distinct = true;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        sum += u[k];
+#pragma unroll
+        for (int j = 0; j < k; ++j) distinct &= u[j] != u[k];
+    }
+    return sum == 45 && distinct;
+}
+
+__global__ __launch_bounds__(256) void check_kernel_i64(const int64_t* __restrict__ boards, uint8_t* __restrict__ out,
+                                                        uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int64_t* b = boards + i * 81;
+        int64_t u[9];
+        bool rows = true, cols = true, boxes = true;
+        for (int r = 0; r < 9 && rows; ++r) {                      // sudoku.py:79-81
+#pragma unroll
+            for (int c = 0; c < 9; ++c) u[c] = b[9 * r + c];
+            rows = unit_ok_i64(u);
+        }
+        for (int c = 0; c < 9 && rows && cols; ++c) {              // sudoku.py:84-86
+#pragma unroll
+            for (int r = 0; r < 9; ++r) u[r] = b[9 * r + c];
+            cols = unit_ok_i64(u);
+        }
+        int64_t box00 = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) box00 += b[9 * (k / 3) + (k % 3)];
+        for (int bx = 0; bx < 9 && rows && cols && boxes; ++bx) {  // sudoku.py:89-92
+            const int r0 = (bx / 3) * 3, c0 = (bx % 3) * 3;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) u[k] = b[9 * (r0 + k / 3) + c0 + k % 3];
+            boxes = unit_ok_i64(u);
+        }
+        uint8_t v = (rows && cols && boxes) ? 1u : 0u;
+        if (rows && cols && box00 == 45) v |= 2u;               // the raw call raises NameError (sudoku.py:68)
+        out[i] = v;
+    }
+}
+
 }  // namespace sdk

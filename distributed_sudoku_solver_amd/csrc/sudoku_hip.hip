@@ -595,6 +595,29 @@ int sdk_check_batch(sdk_ctx* c, const uint8_t* boards, uint8_t* verdict, size_t 
     return SDK_OK;
 }
 
+int sdk_check_batch_i64(sdk_ctx* c, const int64_t* boards, uint8_t* verdict, size_t n) {
+    if (!c || (n && (!boards || !verdict))) return fail(SDK_EINVAL, "NULL argument");
+    if (n == 0) return SDK_OK;
+    for (size_t k = 0; k < n * 81; ++k)
+        if (boards[k] >= (1ll << 59) || boards[k] <= -(1ll << 59))
+            return fail(SDK_EINVAL, "cell value %lld out of the checker's range (|v| < 2^59)", (long long)boards[k]);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure(c->in, n * 81 * sizeof(int64_t))) || (rc = ensure(c->verdict, n))) return rc;
+    HIPCALL(hipMemcpyAsync(c->in.p, boards, n * 81 * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    hipEvent_t stop;
+    if ((rc = timer_begin(c, &stop))) return rc;
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->cus * 8);
+    sdk::check_kernel_i64<<<grid, 256, 0, c->stream>>>(static_cast<const int64_t*>(c->in.p),
+                                                      static_cast<uint8_t*>(c->verdict.p), (uint64_t)n);
+    HIPCALL(hipGetLastError());
+    if ((rc = timer_end(c, stop))) return rc;
+    HIPCALL(hipMemcpyAsync(verdict, c->verdict.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    return SDK_OK;
+}
+
 int sdk_solve_batch(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell_mask, uint8_t* out, int8_t* status,
                     uint64_t* work, size_t n) {
     if (!c || (n && (!in || !out || !status))) return fail(SDK_EINVAL, "NULL argument");

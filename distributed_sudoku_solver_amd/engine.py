@@ -46,18 +46,25 @@ def encode_solve_grid(grid):
     return out
 
 
+CHECK_I64_LIMIT = 1 << 59   # sdk_check_batch_i64: |v| below this keeps a unit's sum exact
+
+
 def encode_check_grid(grid):
-    """9x9 grid -> uint8[81] for the checker (literal sum/set rule needs exact values)."""
+    """9x9 grid -> uint8[81] (every value an integer 0..255) or int64[81] (any integer with
+    |v| < 2^59) for the checker: the literal `sum == 45 and len(set) == 9` rule needs the exact
+    values (5.0 counts as 5, like the reference's `==`).  Non-integral numbers raise ValueError."""
     flat = [v for row in grid for v in row] if len(grid) == 9 else list(grid)
     if len(flat) != 81:
         raise ValueError("a Sudoku grid has 81 cells")
-    out = np.empty(81, dtype=np.uint8)
+    vals = []
     for i, v in enumerate(flat):
         iv = _as_int(v)
-        if iv is None or not 0 <= iv <= 255:
-            raise ValueError(f"cell {i} = {v!r}: the HIP checker takes integers 0..255")
-        out[i] = iv
-    return out
+        if iv is None or not -CHECK_I64_LIMIT < iv < CHECK_I64_LIMIT:
+            raise ValueError(f"cell {i} = {v!r}: the HIP checker takes integers with |v| < 2^59")
+        vals.append(iv)
+    if all(0 <= v <= 255 for v in vals):
+        return np.array(vals, dtype=np.uint8)
+    return np.array(vals, dtype=np.int64)
 
 
 def range_to_mask(arr):
@@ -194,11 +201,14 @@ class SudokuEngine:
 
     # ----------------------------------------------------------- host batch
     def check_batch(self, boards):
-        """uint8[n,81] -> uint8[n] verdict bits (SDK_CHECK_OK | SDK_CHECK_RAW_NAMEERROR)."""
-        boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
+        """uint8[n,81] (or int64[n,81]: sdk_check_batch_i64) -> uint8[n] verdict bits
+        (SDK_CHECK_OK | SDK_CHECK_RAW_NAMEERROR)."""
+        wide = np.asarray(boards).dtype == np.int64
+        boards = np.ascontiguousarray(boards, dtype=np.int64 if wide else np.uint8).reshape(-1, 81)
         n = boards.shape[0]
         verdict = np.empty(n, dtype=np.uint8)
-        L.check(self.lib.sdk_check_batch(self.ctx, _ptr(boards), _ptr(verdict), n), "sdk_check_batch")
+        fn = self.lib.sdk_check_batch_i64 if wide else self.lib.sdk_check_batch
+        L.check(fn(self.ctx, _ptr(boards), _ptr(verdict), n), "sdk_check_batch_i64" if wide else "sdk_check_batch")
         return verdict
 
     def solve_batch(self, boards, masks=None, want_work=False):

@@ -8,8 +8,9 @@ all deliberate:
   * check() returns the INTENDED verdict (each 3x3 box tests its own cells).
     The reference's check() raises NameError whenever rows, columns and the
     box(0,0) sum pass (sudoku.py:68); check(raw=True) reproduces that.
-Grid values must be integers 0..255 (the literal `sum == 45 and len(set) == 9`
-rule is evaluated exactly on that domain).
+Grid values must be integers (|v| < 2^59; 5.0 counts as 5): the literal
+`sum == 45 and len(set) == 9` rule is evaluated exactly -- boards within 0..255
+on the streaming uint8 kernel, others on its int64 twin (sdk_check_batch_i64).
 """
 from .engine import encode_check_grid
 from . import _lib as L

@@ -112,6 +112,10 @@ int sdk_get_option(sdk_ctx *ctx, int key, int64_t *value);
  * `sum == 45 and len(set) == 9`. */
 int sdk_check_batch(sdk_ctx *ctx, const uint8_t *boards, uint8_t *verdict, size_t n);
 
+/* The same for int64 cells (the reference's check() takes any Python int):
+ * |value| < 2^59 (else SDK_EINVAL), so a unit's sum is exact. */
+int sdk_check_batch_i64(sdk_ctx *ctx, const int64_t *boards, uint8_t *verdict, size_t n);
+
 /* Replaces DHTNode.solve_sudoku (DHT_Node.py:474-538) for n boards.
  *   first_cell_mask  nullable; bit d (1..9) = digit d may be tried at the
  *                    lowest-index empty input cell (the TASK `range`); NULL =

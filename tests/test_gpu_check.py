@@ -90,3 +90,32 @@ def test_pipeline_variants_bit_exact(engine, variant):
     finally:
         engine.set_option(L.SDK_OPT_CHECK_VARIANT, L.SDK_CHECK_REG1)
         engine.set_option(L.SDK_OPT_CHECK_BLOCKS_PER_CU, 3)
+
+
+def test_int64_boards_vs_python_restatement(engine):
+    """Out-of-domain ints (the reference's check() takes any Python int): the int64 kernel
+    follows the literal rule, e.g. [0, 2, ..., 8, 10] passes a row (sum 45, 9 distinct)."""
+    from distributed_sudoku_solver_amd.sudoku import Sudoku
+    rng = np.random.default_rng(5)
+    sols, _ = synth.make_check_boards(400, seed=17)
+    boards = sols.astype(np.int64)
+    for i in range(len(boards)):
+        b = boards[i]
+        k = i % 4
+        if k == 0:                                    # swap digits 1 -> 0 and 9 -> 10 (sums stay 45)
+            b[b == 1] = 0
+            b[b == 9] = 10
+        elif k == 1:
+            b[rng.integers(0, 81)] = int(rng.integers(-(1 << 40), 1 << 40))
+        elif k == 2:                                  # shift one digit by +-d and a partner by -+d
+            b[b == 3] = 1000
+            b[b == 4] = -993
+        else:
+            b[rng.integers(0, 81, 3)] = rng.integers(-300, 300, 3)
+    v = engine.check_batch(boards)
+    for b, x in zip(boards, v):
+        raw, intended = O.py_check([int(t) for t in b])
+        assert bool(x & 1) == intended and bool(x & 2) == (raw == "NameError"), b.tolist()
+    assert (v & 1).any() and (v & 2).any()
+    g = [[int(t) for t in boards[0][9 * r: 9 * r + 9]] for r in range(9)]
+    assert Sudoku(g, engine=engine).check() == bool(v[0] & 1)

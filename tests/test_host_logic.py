@@ -19,10 +19,17 @@ def test_encode_solve_grid_follows_reference_equality():
 def test_encode_check_grid_domain():
     g = [[1] * 9 for _ in range(9)]
     g[0][0] = 255
-    assert E.encode_check_grid(g)[0] == 255
-    g[0][0] = 256
-    with pytest.raises(ValueError):
-        E.encode_check_grid(g)
+    b = E.encode_check_grid(g)
+    assert b.dtype == np.uint8 and b[0] == 255
+    g[0][0] = 256                                  # any Python int: the int64 checker path
+    b = E.encode_check_grid(g)
+    assert b.dtype == np.int64 and b[0] == 256
+    g[0][0] = -7.0                                 # 5.0 == 5 in the reference
+    assert E.encode_check_grid(g)[0] == -7
+    for bad in (4.5, 1 << 59, -(1 << 59), "5", None):
+        g[0][0] = bad
+        with pytest.raises(ValueError):
+            E.encode_check_grid(g)
 
 
 def test_range_to_mask_matches_split_semantics():

@@ -10,11 +10,12 @@
 // v_pk_min_u16), so one instruction advances two boards and a propagation round
 // costs about half the VALU instructions per board of solve2's.
 //
-// Cell state, per board (16-bit field):
-//   X  bits 0..8: candidate digits 1..9;  bit 9: out-of-domain given (inert)
-//   S  the digit of a given or of a solved cell (one bit of 0..8), 0 if open;
-//      bit 9 for an inert given
-// so a cell is open (branchable) <=> S == 0; a given is X = S = its digit bit.
+// Cell state, per board (16-bit field), exactly one of X and S is non-zero:
+//   X  candidate digits 1..9 (bits 0..8) of an OPEN cell, 0 once it is closed
+//   S  the digit (one bit of 0..8) of a given or of a solved cell; bit 9 for an
+//      out-of-domain given (inert); 0 while the cell is open
+// so a cell is open (branchable) <=> X != 0, and an open cell that loses its last
+// candidate is X = S = 0 (the contradiction test).
 // Givens are not otherwise marked: what solve2 reads from its "given" field is
 // static per board and kept per unit lane instead, computed once per board by a
 // static pass over the input (start of every board):
@@ -24,24 +25,26 @@
 //      must occur exactly once in every completion), else 0
 // Unit summary (lane j, unit j, both boards): from the 9 cells (X, S) words
 //   T     = OR of S                      (taken digits: givens and solved cells)
-//   once  = X-digits held by exactly one cell, in exact units (hidden singles)
+//   once  = candidates held by exactly one open cell, in exact units (hidden
+//           singles; a digit of T is never applied: every update masks T first)
 //   conflict: a digit taken twice that is not a duplicated given, or an exact
-//             unit that lost a digit.  (A non-given cell can never be solved to
+//             unit that lost a digit (in neither T nor any candidate set).  (A non-given cell can never be solved to
 //             a given digit of its units -- every rule only picks digits outside
 //             T -- so "taken twice, not in D" is solve2's solved-vs-solved /
 //             solved-vs-given test.  The first-cell `range` restriction is the
 //             exception: that cell starts OPEN with X = mask even when the mask
 //             is one digit, so round 1 eliminates T from it like any other cell.)
-// Cell update (open cells): X &= ~T;  hidden single X & once; two hidden singles
-// or no candidate = contradiction; one candidate left -> S = X (solved).
+// Cell update (open cells; a closed cell's X = 0 stays 0): X &= ~T; hidden single
+// X & once; two hidden singles or no candidate = contradiction; one candidate left
+// -> S = that digit, X = 0 (solved).
 //
 // Search per board: as solve2 (events = contradiction or fixpoint; count up to 2
 // completions under MRV, lex re-search when two are found; lowest-open-cell
 // branching under LEX).  A board's search step runs with its 16-bit field pulled
 // out of the packed words; the slot (lo/hi) is a compile-time constant of the step
 // (step4<0>, step4<1>), the two 32-lane halves take their steps under exec masks.
-// DFS snapshot per level: the three X fields of the lane (S is recomputed: at a
-// fixpoint, S = X exactly for the cells with one candidate).
+// DFS snapshot per level: one 16-bit word per cell, X of an open cell or S | 0x400
+// of a closed one.
 #pragma once
 #include "solve2_kernel.h"
 
@@ -158,7 +161,9 @@ struct Cells4 {
     uint32_t D, E;            // statics of the lane's unit (both boards)
 };
 
-// open-cell update of one cell of both boards (see the header)
+// update of one cell of both boards (see the header): a closed cell (X = 0) stays
+// as it is, an open one loses T, takes a hidden single, and closes when one
+// candidate is left
 __device__ __forceinline__ void upd4(uint32_t& X, uint32_t& S, uint32_t U, uint32_t H, uint32_t& bm, uint32_t& zmin,
                                      uint32_t& chg) {
     const uint32_t v1 = X & ~U;
@@ -166,13 +171,12 @@ __device__ __forceinline__ void upd4(uint32_t& X, uint32_t& S, uint32_t U, uint3
     const uint32_t hm = nz16(h);
     const uint32_t v2 = (h & hm) | (v1 & ~hm);
     bm |= h & dec16(h);                           // two hidden singles for one cell
-    const uint32_t om = z16(S);                   // open cells
-    const uint32_t xn = (v2 & om) | (X & ~om);
+    const uint32_t sg = z16(v2 & dec16(v2));      // at most one candidate left
+    const uint32_t xn = v2 & ~sg;
+    S |= v2 & sg;
     zmin = min16(zmin, xn | S);                   // an open cell without candidates
-    const uint32_t add = om & z16(v2 & dec16(v2)) & v2;   // open cell left with one candidate: solved
-    chg |= (xn ^ X) | add;
+    chg |= xn ^ X;                                // S only changes when X does
     X = xn;
-    S |= add;
 }
 
 // One propagation round for all four boards, branch-free.  Out: per-lane packed
@@ -191,7 +195,7 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
         ts |= os & v.y;
         os |= v.y;
     }
-    bm = (ts & ~c.D & kC2) | (c.E & ~ox);
+    bm = (ts & ~c.D & kC2) | (c.E & ~(ox | os));
     w.s_unit[w.hl] = make_uint2(os & kC2, ox & ~tx & c.E);
     __syncthreads();
     const uint2 uc = w.s_unit[w.ucol];
@@ -217,14 +221,20 @@ struct Slot4 {
 };
 
 __device__ __forceinline__ uint32_t cell_x4(uint32_t v) {
-    return v == 0 ? kCands : (v <= 9 ? (1u << (v - 1u)) : kInert4);
+    return v == 0 ? kCands : 0u;
 }
 __device__ __forceinline__ uint32_t cell_s4(uint32_t v) {
     return v == 0 ? 0u : (v <= 9 ? (1u << (v - 1u)) : kInert4);
 }
-// S of a cell restored from a snapshot: its X if one bit is set (given, solved, inert), else open
-__device__ __forceinline__ uint32_t s_of_x4(uint32_t x) {
-    return (x & (x - 1u)) == 0u ? x : 0u;
+// 16-bit snapshot of a cell and back: X if open, S | 0x400 if closed
+__device__ __forceinline__ uint32_t snap4(uint32_t x, uint32_t s) {
+    return x ? x : (s | 0x400u);
+}
+__device__ __forceinline__ uint32_t snap_x4(uint32_t y) {
+    return (y & 0x400u) ? 0u : y;
+}
+__device__ __forceinline__ uint32_t snap_s4(uint32_t y) {
+    return (y & 0x400u) ? (y & 0x3FFu) : 0u;
 }
 
 // kernel arguments as plain values plus the wave's propagation-loop iteration
@@ -251,7 +261,7 @@ __device__ __forceinline__ void start_board4(const Lane4& w, const Args4& a, Slo
         i1 = w.act ? (uint32_t)sin[w.c0 + 27] : 0u;
         i2 = w.act ? (uint32_t)sin[w.c0 + 54] : 0u;
     }
-    uint32_t x0 = w.act ? cell_x4(i0) : kInert4, x1 = w.act ? cell_x4(i1) : kInert4, x2 = w.act ? cell_x4(i2) : kInert4;
+    uint32_t x0 = w.act ? cell_x4(i0) : 0u, x1 = w.act ? cell_x4(i1) : 0u, x2 = w.act ? cell_x4(i2) : 0u;
     const uint32_t s0 = w.act ? cell_s4(i0) : kInert4, s1 = w.act ? cell_s4(i1) : kInert4,
                    s2 = w.act ? cell_s4(i2) : kInert4;
     if (a.mask) {
@@ -316,9 +326,9 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Args4& a, Slot
     if (b.active) {
         start_board4<HI>(w, a, b, c, true);
     } else {
-        c.x0 = setfld<HI>(c.x0, kInert4);
-        c.x1 = setfld<HI>(c.x1, kInert4);
-        c.x2 = setfld<HI>(c.x2, kInert4);
+        c.x0 = setfld<HI>(c.x0, 0u);
+        c.x1 = setfld<HI>(c.x1, 0u);
+        c.x2 = setfld<HI>(c.x2, 0u);
         c.s0 = setfld<HI>(c.s0, kInert4);
         c.s1 = setfld<HI>(c.s1, kInert4);
         c.s2 = setfld<HI>(c.s2, kInert4);
@@ -345,7 +355,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Args4& a, Sl
 }
 
 __device__ __forceinline__ uint32_t branch_key4(uint32_t x, uint32_t s, int cell, int order) {
-    if (s != 0u) return ~0u;
+    if (x == 0u) return ~0u;
     const uint32_t base = ((uint32_t)cell << 9) | x;
     return order == ORDER_LEX ? base : (((uint32_t)__popc(x)) << 16) | base;
 }
@@ -354,11 +364,11 @@ __device__ __forceinline__ uint32_t branch_key4(uint32_t x, uint32_t s, int cell
 template <int HI>
 __device__ __forceinline__ void set_cell4(const Lane4& w, Cells4& c, int cell, uint32_t d) {
     const bool k0 = w.act && cell == w.c0, k1 = w.act && cell == w.c0 + 27, k2 = w.act && cell == w.c0 + 54;
-    c.x0 = k0 ? setfld<HI>(c.x0, d) : c.x0;
+    c.x0 = k0 ? setfld<HI>(c.x0, 0u) : c.x0;
     c.s0 = k0 ? setfld<HI>(c.s0, d) : c.s0;
-    c.x1 = k1 ? setfld<HI>(c.x1, d) : c.x1;
+    c.x1 = k1 ? setfld<HI>(c.x1, 0u) : c.x1;
     c.s1 = k1 ? setfld<HI>(c.s1, d) : c.s1;
-    c.x2 = k2 ? setfld<HI>(c.x2, d) : c.x2;
+    c.x2 = k2 ? setfld<HI>(c.x2, 0u) : c.x2;
     c.s2 = k2 ? setfld<HI>(c.s2, d) : c.s2;
 }
 
@@ -370,7 +380,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
     const uint32_t x0 = fld<HI>(c.x0), x1 = fld<HI>(c.x1), x2 = fld<HI>(c.x2);
     const uint32_t s0 = fld<HI>(c.s0), s1 = fld<HI>(c.s1), s2 = fld<HI>(c.s2);
     int r = bad ? P_CONTRA
-                : (half_any4(w, w.act && (s0 == 0u || s1 == 0u || s2 == 0u)) ? P_OPEN : P_SOLVED);
+                : (half_any4(w, w.act && (x0 | x1 | x2) != 0u) ? P_OPEN : P_SOLVED);
     if (a.budget && b.nodes > a.budget) {
         finish_board4<HI>(w, a, b, c, -2);
         return;
@@ -381,9 +391,9 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
             uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
             const uint8_t* sin = w.s_in + HI * 81;
             const uint32_t i0 = sin[w.c0], i1 = sin[w.c0 + 27], i2 = sin[w.c0 + 54];
-            dst[w.c0] = (uint8_t)(i0 == 0 ? (uint32_t)__ffs(x0) : i0);
-            dst[w.c0 + 27] = (uint8_t)(i1 == 0 ? (uint32_t)__ffs(x1) : i1);
-            dst[w.c0 + 54] = (uint8_t)(i2 == 0 ? (uint32_t)__ffs(x2) : i2);
+            dst[w.c0] = (uint8_t)(i0 == 0 ? (uint32_t)__ffs(s0) : i0);
+            dst[w.c0 + 27] = (uint8_t)(i1 == 0 ? (uint32_t)__ffs(s1) : i1);
+            dst[w.c0 + 54] = (uint8_t)(i2 == 0 ? (uint32_t)__ffs(s2) : i2);
         }
         if (b.count >= b.lim) {
             if (b.order == ORDER_MRV) {      // >= 2 completions: lex re-search
@@ -407,7 +417,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
         const int cell = (int)((key >> 9) & 0x7Fu);
         const uint32_t m = key & kCands;
         const uint32_t d = m & (0u - m);
-        const uint2 snap = make_uint2(x0 | (x1 << 16), x2);
+        const uint2 snap = make_uint2(snap4(x0, s0) | (snap4(x1, s1) << 16), snap4(x2, s2));
         if (b.depth < kLds4Levels) s_stk[b.depth][HI][w.lane] = snap;
         else g_stk[(b.depth * 2 + HI) * 64 + w.lane] = snap;
         if (w.hl == 0) br[b.depth] = (uint32_t)cell | ((m ^ d) << 16);
@@ -429,12 +439,12 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
     const uint2 snap =
         b.depth - 1 < kLds4Levels ? s_stk[b.depth - 1][HI][w.lane] : g_stk[((b.depth - 1) * 2 + HI) * 64 + w.lane];
     const uint32_t y0 = snap.x & 0xFFFFu, y1 = snap.x >> 16, y2 = snap.y;
-    c.x0 = setfld<HI>(c.x0, y0);
-    c.x1 = setfld<HI>(c.x1, y1);
-    c.x2 = setfld<HI>(c.x2, y2);
-    c.s0 = setfld<HI>(c.s0, s_of_x4(y0));
-    c.s1 = setfld<HI>(c.s1, s_of_x4(y1));
-    c.s2 = setfld<HI>(c.s2, s_of_x4(y2));
+    c.x0 = setfld<HI>(c.x0, snap_x4(y0));
+    c.x1 = setfld<HI>(c.x1, snap_x4(y1));
+    c.x2 = setfld<HI>(c.x2, snap_x4(y2));
+    c.s0 = setfld<HI>(c.s0, snap_s4(y0));
+    c.s1 = setfld<HI>(c.s1, snap_s4(y1));
+    c.s2 = setfld<HI>(c.s2, snap_s4(y2));
     if (rest == 0) --b.depth;
     else if (w.hl == 0) br[b.depth - 1] = (uint32_t)cell | (rest << 16);
     set_cell4<HI>(w, c, cell, d);
@@ -492,7 +502,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     a.iter = 0;
 
     Cells4 c;
-    c.x0 = c.x1 = c.x2 = c.s0 = c.s1 = c.s2 = kInert4x2;
+    c.x0 = c.x1 = c.x2 = 0u;
+    c.s0 = c.s1 = c.s2 = kInert4x2;
     c.D = 0;
     c.E = 0;
     bool act0 = first_board4<0>(w, a, c, s_slot);

@@ -74,7 +74,7 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=20250614)
     ap.add_argument("--c2-puzzles", type=int, default=1_000_000,
                     help="C2 leg: ~30-clue unique puzzles per GPU (0 = skip)")
-    ap.add_argument("--minimal-puzzles", type=int, default=65536,
+    ap.add_argument("--minimal-puzzles", type=int, default=1 << 20,
                     help="distinct minimal-puzzle leg, puzzles per GPU (0 = skip)")
     ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
@@ -317,7 +317,7 @@ def minimal_leg(eng, d, args, synth, L):
     the completion stays unique, 21-29 clues; csrc/gen_minimal.c), resident in HBM, checked against
     their generating grids, with the search-tail statistics (nodes, max DFS depth) of the same set."""
     n = args.minimal_puzzles
-    p, s = synth.make_minimal(n, lo=d.rank * n, threads=cpu_share())
+    p, s = synth.make_minimal_sym(n, base=65536, lo=d.rank * 65536, threads=cpu_share())
     el, k_s, bad = solve_leg(eng, d, args, p, s, 3, 1)
     stats = {}
     for kind, name in ((L.SDK_WORK_NODES, "nodes"), (L.SDK_WORK_ROUNDS, "rounds"), (L.SDK_WORK_DEPTH, "depth")):
@@ -326,8 +326,8 @@ def minimal_leg(eng, d, args, synth, L):
         stats[name] = {"mean": float(w.mean()), "p50": float(np.percentile(w, 50)),
                        "p99": float(np.percentile(w, 99)), "max": int(w.max())}
     eng.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
-    return {"workload": f"{n} distinct minimal unique puzzles per GPU (random grids, {int((p > 0).sum(1).mean())} "
-                        "clues on average)",
+    return {"workload": f"{n} minimal unique puzzles per GPU: 65536 distinct random-grid puzzles "
+                        f"({int((p > 0).sum(1).mean())} clues on average) x seeded symmetries",
             "value": d.world * n * 3 / el, "unit": "puzzles/s", "avg_kernel_ms": k_s * 1000.0,
             "search": stats, "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
 

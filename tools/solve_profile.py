@@ -20,11 +20,16 @@ ap.add_argument("--stats", action="store_true")
 ap.add_argument("--waves-per-cu", type=int, default=0)
 ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave", "quad"])
 ap.add_argument("--sweep", action="store_true", help="time waves-per-CU settings")
+ap.add_argument("--order", default="mrv_unique", choices=["mrv_unique", "lex"])
 args = ap.parse_args()
 
-gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
-p, s = gen(args.n, seed=11)
+if args.workload == "minimal":
+    p, s = synth.make_minimal_sym(args.n, threads=16)
+else:
+    gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
+    p, s = gen(args.n, seed=11)
 with SudokuEngine(0) as eng:
+    eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
     eng.set_option(L.SDK_OPT_SOLVER, {"halfwave": L.SDK_SOLVER_HALFWAVE, "wave": L.SDK_SOLVER_WAVE,
                                       "quad": L.SDK_SOLVER_QUAD}[args.solver])
     wopt = L.SDK_OPT_WAVES_PER_CU if args.solver == "wave" else L.SDK_OPT_WAVES_PER_CU2
@@ -41,7 +46,7 @@ with SudokuEngine(0) as eng:
     ms, nl = eng.timer_read()
     out = np.empty((args.n, 81), np.uint8)
     d_out.download(out)
-    print(f"{args.solver} {args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
+    print(f"{args.solver} {args.order} {args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
           f"ok={(out == s).all()}", flush=True)
     if args.sweep:
         for wpc in (8, 12, 16, 20, 24, 32):

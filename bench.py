@@ -60,7 +60,7 @@ def parse_args():
     ap.add_argument("--check-steps", type=int, default=10)
     ap.add_argument("--check-warmup", type=int, default=10,
                     help="untimed checker launches first (the memory clocks ramp under sustained streaming)")
-    ap.add_argument("--order", choices=["mrv_unique", "lex"], default="mrv_unique")
+    ap.add_argument("--order", choices=["mrv_unique", "lex"], default="lex")
     ap.add_argument("--solver", choices=sorted(SOLVERS), default="quad",
                     help="solve kernel: four boards per wave (solve4_kernel), two (solve2_kernel) or one (solve_kernel)")
     ap.add_argument("--waves-per-cu", type=int, default=None)

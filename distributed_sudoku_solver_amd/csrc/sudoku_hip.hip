@@ -64,7 +64,7 @@ struct sdk_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // options
-    int order = SDK_ORDER_MRV_UNIQUE;
+    int order = SDK_ORDER_LEX;     // lex-first DFS: no uniqueness proof needed (faster than MRV_UNIQUE, r02)
     uint64_t budget = 0;
     int waves_per_cu = 32;
     int check_blocks_per_cu = 3;

@@ -62,7 +62,7 @@ extern "C" {
                                    /* (sudoku.py:68): rows ok, cols ok, box00 sum 45 */
 
 /* options for sdk_set_option */
-#define SDK_OPT_ORDER        1  /* SDK_ORDER_*                                        */
+#define SDK_OPT_ORDER        1  /* SDK_ORDER_* (default LEX)                           */
 #define SDK_OPT_NODE_BUDGET  2  /* max search nodes per board, 0 = unlimited          */
 #define SDK_OPT_WAVES_PER_CU 3  /* solver residency, 1..32 (default 32)               */
 #define SDK_OPT_CHECK_BLOCKS_PER_CU 4 /* checker grid = CUs x this, 1..16 (default 3)  */

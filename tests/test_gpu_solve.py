@@ -22,7 +22,7 @@ def ordered_engine(request, engine):
     engine.set_option(L.SDK_OPT_SOLVER, solver)
     engine.set_option(L.SDK_OPT_ORDER, order)
     yield engine
-    engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+    engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
     engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
 
 
@@ -148,7 +148,7 @@ def test_lex_and_mrv_orders_agree_on_seeds(solver_engine):
         engine.set_option(L.SDK_OPT_ORDER, order)
         out, st, _ = engine.solve_batch(p)
         assert (st == 1).all() and (out == s).all()
-    engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+    engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
 
 
 def test_unsolvable_and_edge_boards(solver_engine):
@@ -415,7 +415,7 @@ def test_minimal_unique_puzzles_100k(engine):
             assert depth.max() > 10, (solver, int(depth.max()))
     finally:
         engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
-        engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+        engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
         engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
 
 

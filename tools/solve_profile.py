@@ -20,7 +20,7 @@ ap.add_argument("--stats", action="store_true")
 ap.add_argument("--waves-per-cu", type=int, default=0)
 ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave", "quad"])
 ap.add_argument("--sweep", action="store_true", help="time waves-per-CU settings")
-ap.add_argument("--order", default="mrv_unique", choices=["mrv_unique", "lex"])
+ap.add_argument("--order", default="lex", choices=["mrv_unique", "lex"])
 args = ap.parse_args()
 
 if args.workload == "minimal":

@@ -106,9 +106,11 @@ __device__ __forceinline__ uint32_t setfld(uint32_t w, uint32_t v) {
 // Lane layout (solve2's).  Every lane, spare lanes 27..31 included, owns cells
 // c0, c0+27, c0+54 and reads the unit summaries ucol, ur0 + {0,3,6}, ub0 + {0,3,6},
 // so each group of three LDS accesses is one base register plus immediate offsets.
-// Spare lanes own the inert slots 81+e, 108+e, 135+e and read lane 0's units (their
-// cells are never open, so what they read does not matter; same addresses = broadcast).
-constexpr int kCells4 = 140;                          // LDS cell slots per half
+// Spare lanes own the inert slots 91+e, 118+e, 145+e -- banks that no real cell of the
+// same ds_write_b64 lane group uses (tools/lds_banks.py: no conflict in any access of a
+// round) -- and read lane 0's units (their cells are never open, so what they read
+// does not matter; same addresses = broadcast).
+constexpr int kCells4 = 150;                          // LDS cell slots per half
 struct Lane4 {
     int lane, hl, half;
     bool act;
@@ -128,7 +130,7 @@ __device__ __forceinline__ void init_lane4(Lane4& w, uint2* s_cell_all, uint2* s
     w.half = l2.half;
     w.act = l2.act;
     const int j = w.act ? w.hl : 0;
-    w.c0 = w.act ? j : 81 + (w.hl - 27);
+    w.c0 = w.act ? j : 91 + (w.hl - 27);
     w.ucol = 9 + j % 9;
     w.ur0 = j / 9;
     w.ub0 = 18 + (j % 9) / 3;

@@ -23,6 +23,7 @@ a GPU-backed node) and the CPU baseline (rank 0, N=1 only): the oracle's C port 
 the reference's naive DFS on a bounded sample of the same puzzles.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -430,7 +431,10 @@ def main():
         mod, fn = args.engine_factory.split(":")
         eng = getattr(importlib.import_module(mod), fn)(d.local_rank)
     else:
-        eng = SudokuEngine(d.local_rank)
+        # one GPU per rank; more ranks than GPUs (a 1-GPU rehearsal of the rank path) share them
+        ndev = ctypes.c_int(0)
+        L.check(L.load().sdk_device_count(ctypes.byref(ndev)), "sdk_device_count")
+        eng = SudokuEngine(d.local_rank % max(1, ndev.value))
     eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
     eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
     if args.waves_per_cu:

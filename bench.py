@@ -96,7 +96,17 @@ class Dist:
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            # gloo prints its connection log on the process's stdout; rank 0's stdout must be
+            # exactly the one JSON line, so fd 1 points at stderr while the group forms
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):

@@ -152,8 +152,10 @@ __device__ __forceinline__ uint32_t half_first4(const Lane4& w, uint32_t v) {
 
 // a wave-uniform 64-bit lane mask with every 32-lane half that has a set bit filled
 __device__ __forceinline__ uint64_t spread_halves(uint64_t m) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)m) != 0u ? 0xFFFFFFFFu : 0u;
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) != 0u ? 0xFFFFFFFFu : 0u;
+    // scalar compare/select (clang otherwise rebuilds this as 64-bit VALU compares)
+    uint32_t lo, hi;
+    asm("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, -1, 0" : "=s"(lo) : "s"((uint32_t)m) : "scc");
+    asm("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, -1, 0" : "=s"(hi) : "s"((uint32_t)(m >> 32)) : "scc");
     return ((uint64_t)hi << 32) | lo;
 }
 
@@ -508,15 +510,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     c.s0 = c.s1 = c.s2 = kInert4x2;
     c.D = 0;
     c.E = 0;
-    bool act0 = first_board4<0>(w, a, c, s_slot);
-    bool act1 = first_board4<1>(w, a, c, s_slot);
+    const bool act0 = first_board4<0>(w, a, c, s_slot);
+    const bool act1 = first_board4<1>(w, a, c, s_slot);
 
     // Event detection in scalar registers: one ballot per (flag, slot), each spread
     // to the 32 lanes of the half it came from; a slot's board takes its search step
-    // when it contradicted (B) or nothing changed (no C) in its half.
-    for (;;) {
-        const uint64_t A0 = __builtin_amdgcn_ballot_w64(act0), A1 = __builtin_amdgcn_ballot_w64(act1);
-        if ((A0 | A1) == 0) break;
+    // when it contradicted (B) or nothing changed (no C) in its half.  A* = halves
+    // whose slot still has a board.
+    uint64_t A0 = __builtin_amdgcn_ballot_w64(act0), A1 = __builtin_amdgcn_ballot_w64(act1);
+    while ((A0 | A1) != 0) {
         uint32_t bm, zmin, chg;
         round4(w, c, bm, zmin, chg);
         ++a.iter;
@@ -526,10 +528,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
         const uint64_t C0 = spread_halves(__builtin_amdgcn_ballot_w64((chg & 0xFFFFu) != 0u));
         const uint64_t C1 = spread_halves(__builtin_amdgcn_ballot_w64(chg > 0xFFFFu));
         const uint64_t E0 = A0 & (B0 | ~C0), E1 = A1 & (B1 | ~C1);
-        if (E0 != 0 && __builtin_amdgcn_inverse_ballot_w64(E0))
-            act0 = step4<0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_br, s_stk, g_stk, s_slot);
-        if (E1 != 0 && __builtin_amdgcn_inverse_ballot_w64(E1))
-            act1 = step4<1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_br, s_stk, g_stk, s_slot);
+        if (E0 != 0) {
+            bool r = false;
+            if (__builtin_amdgcn_inverse_ballot_w64(E0))
+                r = step4<0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_br, s_stk, g_stk, s_slot);
+            A0 = (A0 & ~E0) | (__builtin_amdgcn_ballot_w64(r) & E0);
+        }
+        if (E1 != 0) {
+            bool r = false;
+            if (__builtin_amdgcn_inverse_ballot_w64(E1))
+                r = step4<1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_br, s_stk, g_stk, s_slot);
+            A1 = (A1 & ~E1) | (__builtin_amdgcn_ballot_w64(r) & E1);
+        }
     }
 }
 #endif  // SDK_DEFINE_SOLVE4_KERNEL

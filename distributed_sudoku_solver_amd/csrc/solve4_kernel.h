@@ -20,7 +20,8 @@
 // static per board and kept per unit lane instead, computed once per board by a
 // static pass over the input (start of every board):
 //   D  digits given at least twice in the unit (given-vs-given duplicates: the
-//      reference never validates clues, SURVEY §0.9, so they are no conflict)
+//      reference never validates clues, SURVEY §0.9, so they are no conflict);
+//      Cells4::D holds its complement within the candidate bits, kC2 & ~D
 //   E  0x1FF if the unit is exact (no duplicate and no inert given: every digit
 //      must occur exactly once in every completion), else 0
 // Unit summary (lane j, unit j, both boards): from the 9 cells (X, S) words
@@ -162,25 +163,83 @@ __device__ __forceinline__ uint64_t spread_halves(uint64_t m) {
 // packed lane state: the lane's three cells of both boards of its half
 struct Cells4 {
     uint32_t x0, x1, x2, s0, s1, s2;
-    uint32_t D, E;            // statics of the lane's unit (both boards)
+    uint32_t D, E;            // statics of the lane's unit (both boards); D as kC2 & ~D
 };
 
 // update of one cell of both boards (see the header): a closed cell (X = 0) stays
 // as it is, an open one loses T, takes a hidden single, and closes when one
-// candidate is left
-__device__ __forceinline__ void upd4(uint32_t& X, uint32_t& S, uint32_t U, uint32_t H, uint32_t& bm, uint32_t& zmin,
+// candidate is left.  One asm block (v_bitop3_b32 truth tables over S0 = 0xF0,
+// S1 = 0xCC, S2 = 0xAA): split into separate statements, every packed op becomes
+// its own asm statement and clang pads each one's consumer with an s_nop.
+//   v1 = X & ~U              h  = v1 & H           hm = nz16(h)
+//   v2 = h | (v1 & ~hm)      (the hidden single, or what is left)
+//   bm |= h & dec16(h)       (two hidden singles for one cell)
+//   sg = z16(v2 & dec16(v2)) (at most one candidate left)
+//   m  = v2 | S              (0 in a half: an open cell without candidates)
+//   S |= v2 & sg             Xn = v2 & ~sg          chg |= X ^ Xn
+__device__ __forceinline__ void upd4(uint32_t& X, uint32_t& S, uint32_t U, uint32_t H, uint32_t& bm, uint32_t& m,
                                      uint32_t& chg) {
-    const uint32_t v1 = X & ~U;
-    const uint32_t h = v1 & H;
-    const uint32_t hm = nz16(h);
-    const uint32_t v2 = (h & hm) | (v1 & ~hm);
-    bm |= h & dec16(h);                           // two hidden singles for one cell
-    const uint32_t sg = z16(v2 & dec16(v2));      // at most one candidate left
-    const uint32_t xn = v2 & ~sg;
-    S |= v2 & sg;
-    zmin = min16(zmin, xn | S);                   // an open cell without candidates
-    chg |= xn ^ X;                                // S only changes when X does
+    uint32_t xn, v1, h, t, v2;
+    asm("v_bitop3_b32 %[v1], %[x], %[u], %[u] bitop3:0x30\n\t"
+        "v_and_b32 %[h], %[v1], %[hh]\n\t"
+        "v_pk_sub_u16 %[t], 0, %[h]\n\t"
+        "v_pk_ashrrev_i16 %[t], 15, %[t] op_sel_hi:[0,1]\n\t"
+        "v_bitop3_b32 %[v2], %[h], %[v1], %[t] bitop3:0xf4\n\t"
+        "v_pk_add_u16 %[t], %[h], -1\n\t"
+        "v_and_or_b32 %[bm], %[h], %[t], %[bm]\n\t"
+        "v_pk_add_u16 %[t], %[v2], -1\n\t"
+        "v_and_b32 %[t], %[v2], %[t]\n\t"
+        "v_or_b32 %[m], %[v2], %[s]\n\t"
+        "v_pk_add_u16 %[t], %[t], -1\n\t"
+        "v_pk_ashrrev_i16 %[t], 15, %[t] op_sel_hi:[0,1]\n\t"
+        "v_and_or_b32 %[s], %[v2], %[t], %[s]\n\t"
+        "v_bitop3_b32 %[xn], %[v2], %[t], %[t] bitop3:0x30\n\t"
+        "v_bitop3_b32 %[chg], %[chg], %[x], %[xn] bitop3:0xf6"
+        : [xn] "=&v"(xn), [v1] "=&v"(v1), [h] "=&v"(h), [t] "=&v"(t), [v2] "=&v"(v2), [m] "=&v"(m),
+          [s] "+v"(S), [bm] "+v"(bm), [chg] "+v"(chg)
+        : [x] "v"(X), [u] "v"(U), [hh] "v"(H));
     X = xn;
+}
+
+// Unit summary of the lane's unit from its nine (X, S) cell words, one asm block.
+// "In two or more cells" is accumulated two cells at a time: a bit is set in at
+// least two of (acc, a, b) exactly when it is in their majority (bitop3 0xe8).
+//   once = OR X & ~twice(X) & E            T = OR S & kC2
+//   bm   = (twice(S) & Dn) | (E & ~(OR X | OR S))      (Dn = kC2 & ~D of the header)
+__device__ __forceinline__ void unit4(const uint2 (&v)[9], uint32_t E, uint32_t Dn, uint32_t& once, uint32_t& T,
+                                      uint32_t& bm) {
+    uint32_t ox, os, t0, t1, t2, t3;
+    asm("v_or3_b32 %[ox], %[a0], %[a1], %[a2]\n\t"
+        "v_bitop3_b32 %[t0], %[a0], %[a1], %[a2] bitop3:0xe8\n\t"
+        "v_bitop3_b32 %[t1], %[ox], %[a3], %[a4] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a3], %[a4]\n\t"
+        "v_bitop3_b32 %[t2], %[ox], %[a5], %[a6] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a5], %[a6]\n\t"
+        "v_bitop3_b32 %[t3], %[ox], %[a7], %[a8] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a7], %[a8]\n\t"
+        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        "v_bitop3_b32 %[t0], %[ox], %[t0], %[t3] bitop3:0x10\n\t"
+        "v_and_b32 %[once], %[t0], %[e]\n\t"
+        "v_or3_b32 %[os], %[b0], %[b1], %[b2]\n\t"
+        "v_bitop3_b32 %[t0], %[b0], %[b1], %[b2] bitop3:0xe8\n\t"
+        "v_bitop3_b32 %[t1], %[os], %[b3], %[b4] bitop3:0xe8\n\t"
+        "v_or3_b32 %[os], %[os], %[b3], %[b4]\n\t"
+        "v_bitop3_b32 %[t2], %[os], %[b5], %[b6] bitop3:0xe8\n\t"
+        "v_or3_b32 %[os], %[os], %[b5], %[b6]\n\t"
+        "v_bitop3_b32 %[t3], %[os], %[b7], %[b8] bitop3:0xe8\n\t"
+        "v_or3_b32 %[os], %[os], %[b7], %[b8]\n\t"
+        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        "v_bitop3_b32 %[t0], %[t0], %[t3], %[dn] bitop3:0xa8\n\t"
+        "v_bitop3_b32 %[t1], %[e], %[ox], %[os] bitop3:0x10\n\t"
+        "v_or_b32 %[bm], %[t0], %[t1]\n\t"
+        "v_and_b32 %[tt], 0x1ff01ff, %[os]"
+        : [ox] "=&v"(ox), [os] "=&v"(os), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [once] "=&v"(once), [bm] "=&v"(bm), [tt] "=&v"(T)
+        : [a0] "v"(v[0].x), [a1] "v"(v[1].x), [a2] "v"(v[2].x), [a3] "v"(v[3].x), [a4] "v"(v[4].x),
+          [a5] "v"(v[5].x), [a6] "v"(v[6].x), [a7] "v"(v[7].x), [a8] "v"(v[8].x),
+          [b0] "v"(v[0].y), [b1] "v"(v[1].y), [b2] "v"(v[2].y), [b3] "v"(v[3].y), [b4] "v"(v[4].y),
+          [b5] "v"(v[5].y), [b6] "v"(v[6].y), [b7] "v"(v[7].y), [b8] "v"(v[8].y),
+          [e] "v"(E), [dn] "v"(Dn));
 }
 
 // One propagation round for all four boards, branch-free.  Out: per-lane packed
@@ -190,26 +249,22 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
     w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
     w.s_cell[w.c0 + 54] = make_uint2(c.x2, c.s2);
     __syncthreads();
-    uint32_t ox = 0, tx = 0, os = 0, ts = 0;
+    uint2 v[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const uint2 v = w.s_cell[w.ucell[k]];
-        tx |= ox & v.x;
-        ox |= v.x;
-        ts |= os & v.y;
-        os |= v.y;
-    }
-    bm = (ts & ~c.D & kC2) | (c.E & ~(ox | os));
-    w.s_unit[w.hl] = make_uint2(os & kC2, ox & ~tx & c.E);
+    for (int k = 0; k < 9; ++k) v[k] = w.s_cell[w.ucell[k]];
+    uint32_t once, T;
+    unit4(v, c.E, c.D, once, T, bm);
+    w.s_unit[w.hl] = make_uint2(T, once);
     __syncthreads();
     const uint2 uc = w.s_unit[w.ucol];
     const uint2 r0 = w.s_unit[w.ur0], r1 = w.s_unit[w.ur0 + 3], r2 = w.s_unit[w.ur0 + 6];
     const uint2 b0 = w.s_unit[w.ub0], b1 = w.s_unit[w.ub0 + 3], b2 = w.s_unit[w.ub0 + 6];
-    zmin = 0xFFFFFFFFu;
+    uint32_t m0, m1, m2;
     chg = 0;
-    upd4(c.x0, c.s0, uc.x | r0.x | b0.x, uc.y | r0.y | b0.y, bm, zmin, chg);
-    upd4(c.x1, c.s1, uc.x | r1.x | b1.x, uc.y | r1.y | b1.y, bm, zmin, chg);
-    upd4(c.x2, c.s2, uc.x | r2.x | b2.x, uc.y | r2.y | b2.y, bm, zmin, chg);
+    upd4(c.x0, c.s0, uc.x | r0.x | b0.x, uc.y | r0.y | b0.y, bm, m0, chg);
+    upd4(c.x1, c.s1, uc.x | r1.x | b1.x, uc.y | r1.y | b1.y, bm, m1, chg);
+    upd4(c.x2, c.s2, uc.x | r2.x | b2.x, uc.y | r2.y | b2.y, bm, m2, chg);
+    zmin = min16(min16(m0, m1), m2);
 }
 
 // per-slot search state, uniform within the half.  It lives in LDS between steps
@@ -307,7 +362,7 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
     __syncthreads();   // the next round's stores must not overtake these reads
     const uint32_t dup = ts & kCands;
     const uint32_t exact = (dup == 0u && (os & kInert4) == 0u) ? kCands : 0u;
-    c.D = setfld<HI>(c.D, dup);
+    c.D = setfld<HI>(c.D, kCands & ~dup);
     c.E = setfld<HI>(c.E, exact);
 }
 
@@ -508,7 +563,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     Cells4 c;
     c.x0 = c.x1 = c.x2 = 0u;
     c.s0 = c.s1 = c.s2 = kInert4x2;
-    c.D = 0;
+    c.D = kC2;
     c.E = 0;
     const bool act0 = first_board4<0>(w, a, c, s_slot);
     const bool act1 = first_board4<1>(w, a, c, s_slot);

@@ -52,14 +52,17 @@
 namespace sdk {
 
 #ifndef SDK_SOLVE4_LDS_LEVELS
-#define SDK_SOLVE4_LDS_LEVELS 2
+#define SDK_SOLVE4_LDS_LEVELS 0
 #endif
 #ifndef SDK_SOLVE4_WAVES_PER_EU
-#define SDK_SOLVE4_WAVES_PER_EU 6
+#define SDK_SOLVE4_WAVES_PER_EU 7
 #endif
 // DFS levels kept in LDS (per level: 2 slots x 64 lanes x 8 B = 1 KiB; deeper levels go
-// to the per-workgroup global stack).  2 levels keep the block at 6.6 KiB, so 24 waves
-// (6 per SIMD at 80 VGPRs) fit a CU's 160 KiB.
+// to the per-workgroup global stack).  Default 0: a 17-clue board branches 1.65 times
+// on average, so the stack is cold, and the 4.4 KiB block lets occupancy follow the
+// VGPR budget -- 7 waves per SIMD at 72 VGPRs measured best (4M 17-clue puzzles:
+// 2 levels / 6 waves 692M/s, 0 / 7 731M/s, 0 / 8 715M/s, the last spilling outside
+// the round).
 constexpr int kLds4Levels = SDK_SOLVE4_LDS_LEVELS;
 constexpr int kStack4WordsPerBlock = kMaxDepth * 2 * 64 * 2;
 constexpr uint32_t kC2 = 0x01FF01FFu;                 // candidate bits of both boards
@@ -112,18 +115,24 @@ __device__ __forceinline__ uint32_t setfld(uint32_t w, uint32_t v) {
 // round) -- and read lane 0's units (their cells are never open, so what they read
 // does not matter; same addresses = broadcast).
 constexpr int kCells4 = 150;                          // LDS cell slots per half
+// Unit words follow the cells in the same per-half region: unit u at slot kCells4 + u,
+// and every lane writes its unit word kCells4 slots past its first cell's slot (spare
+// lanes into kCells4 + 91..95, read by nobody), so the cell stores and the unit store
+// share one address register.  Same banks as separate arrays: the half stride,
+// 2 * kRegion4 dwords, is 44 mod 64 like the cells' own 2 * kCells4.
+constexpr int kRegion4 = kCells4 + 96;
 struct Lane4 {
     int lane, hl, half;
     bool act;
     int c0;
     int ucol, ur0, ub0;
     int ucell[9];
-    uint2* s_cell;            // this half's kCells4 (X, S) words
+    uint2* s_cell;            // this half's kCells4 (X, S) words, then its units
     uint2* s_unit;            // this half's 32 (T, once) words
     uint8_t* s_in;            // this half's input bytes, [slot][81]
 };
 
-__device__ __forceinline__ void init_lane4(Lane4& w, uint2* s_cell_all, uint2* s_unit_all, uint8_t* s_in_all) {
+__device__ __forceinline__ void init_lane4(Lane4& w, uint2* s_region_all, uint8_t* s_in_all) {
     Lane2 l2;
     init_lane2(l2, nullptr, nullptr);
     w.lane = l2.lane;
@@ -137,8 +146,8 @@ __device__ __forceinline__ void init_lane4(Lane4& w, uint2* s_cell_all, uint2* s
     w.ub0 = 18 + (j % 9) / 3;
 #pragma unroll
     for (int k = 0; k < 9; ++k) w.ucell[k] = l2.ucell[k];
-    w.s_cell = s_cell_all + w.half * kCells4;
-    w.s_unit = s_unit_all + w.half * 32;
+    w.s_cell = s_region_all + w.half * kRegion4;
+    w.s_unit = w.s_cell + kCells4;
     w.s_in = s_in_all + w.half * 2 * 81;
 }
 
@@ -254,7 +263,7 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
     for (int k = 0; k < 9; ++k) v[k] = w.s_cell[w.ucell[k]];
     uint32_t once, T;
     unit4(v, c.E, c.D, once, T, bm);
-    w.s_unit[w.hl] = make_uint2(T, once);
+    w.s_unit[w.c0] = make_uint2(T, once);
     __syncthreads();
     const uint2 uc = w.s_unit[w.ucol];
     const uint2 r0 = w.s_unit[w.ur0], r1 = w.s_unit[w.ur0 + 3], r2 = w.s_unit[w.ur0 + 6];
@@ -419,6 +428,40 @@ __device__ __forceinline__ uint32_t branch_key4(uint32_t x, uint32_t s, int cell
     return order == ORDER_LEX ? base : (((uint32_t)__popc(x)) << 16) | base;
 }
 
+// LEX branch cell of each half without a cross-lane reduction: lane j < 27 owns
+// cells j, j + 27, j + 54, so the lowest open cell is the first lane whose first
+// cell is open, else the first whose second is, else the first whose third is --
+// three ballots and scalar bit scans; its candidates come back by v_readlane.
+// (Spare lanes' cells are never open.)  Out: the cell and its candidate mask for
+// the lane's half; a half outside EXEC gets junk nobody reads.
+__device__ __forceinline__ void lex_pick4(const Lane4& w, uint32_t x0, uint32_t x1, uint32_t x2, int& cell,
+                                          uint32_t& m) {
+    const uint64_t o0 = __builtin_amdgcn_ballot_w64(x0 != 0u);
+    const uint64_t o1 = __builtin_amdgcn_ballot_w64(x1 != 0u);
+    const uint64_t o2 = __builtin_amdgcn_ballot_w64(x2 != 0u);
+    uint32_t cl[2], ml[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t a0 = (uint32_t)(o0 >> (32 * h)), a1 = (uint32_t)(o1 >> (32 * h)),
+                       a2 = (uint32_t)(o2 >> (32 * h));
+        if (a0 != 0u) {
+            const uint32_t l = __builtin_ctz(a0);
+            cl[h] = l;
+            ml[h] = __builtin_amdgcn_readlane(x0, 32 * h + l);
+        } else if (a1 != 0u) {
+            const uint32_t l = __builtin_ctz(a1);
+            cl[h] = 27 + l;
+            ml[h] = __builtin_amdgcn_readlane(x1, 32 * h + l);
+        } else {
+            const uint32_t l = a2 != 0u ? __builtin_ctz(a2) : 0u;
+            cl[h] = 54 + l;
+            ml[h] = __builtin_amdgcn_readlane(x2, 32 * h + l);
+        }
+    }
+    cell = (int)(w.half ? cl[1] : cl[0]);
+    m = w.half ? ml[1] : ml[0];
+}
+
 // branch-free (selects): see solve2's set_cell2 on guarded updates of the three cells
 template <int HI>
 __device__ __forceinline__ void set_cell4(const Lane4& w, Cells4& c, int cell, uint32_t d) {
@@ -432,8 +475,11 @@ __device__ __forceinline__ void set_cell4(const Lane4& w, Cells4& c, int cell, u
 }
 
 // the search step of the board in slot HI after its round ended (bad: contradiction)
+// DFS level record: every lane keeps the level's branch record -- cell | untried
+// digits << 7, uniform in the half -- in the free upper 16 bits of its own snapshot
+// word y, so a level is one 8-byte word per lane and needs no shared record array.
 template <int HI>
-__device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4& b, Cells4& c, bool bad, uint32_t* s_br,
+__device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4& b, Cells4& c, bool bad,
                                            uint2 (*s_stk)[2][64], uint2* g_stk) {
     ++b.nodes;
     const uint32_t x0 = fld<HI>(c.x0), x1 = fld<HI>(c.x1), x2 = fld<HI>(c.x2);
@@ -466,20 +512,25 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
         }
         r = P_CONTRA;
     }
-    uint32_t* br = s_br + (w.half * 2 + HI) * kMaxDepth;
     if (r == P_OPEN) {
-        uint32_t key = ~0u;
-        if (w.act)
-            key = min(branch_key4(x0, s0, w.c0, b.order),
-                      min(branch_key4(x1, s1, w.c0 + 27, b.order), branch_key4(x2, s2, w.c0 + 54, b.order)));
-        key = half_min(key);
-        const int cell = (int)((key >> 9) & 0x7Fu);
-        const uint32_t m = key & kCands;
+        int cell;
+        uint32_t m;
+        if (b.order == ORDER_LEX) {
+            lex_pick4(w, x0, x1, x2, cell, m);
+        } else {
+            uint32_t key = ~0u;
+            if (w.act)
+                key = min(branch_key4(x0, s0, w.c0, b.order),
+                          min(branch_key4(x1, s1, w.c0 + 27, b.order), branch_key4(x2, s2, w.c0 + 54, b.order)));
+            key = half_min(key);
+            cell = (int)((key >> 9) & 0x7Fu);
+            m = key & kCands;
+        }
         const uint32_t d = m & (0u - m);
-        const uint2 snap = make_uint2(snap4(x0, s0) | (snap4(x1, s1) << 16), snap4(x2, s2));
+        const uint2 snap = make_uint2(snap4(x0, s0) | (snap4(x1, s1) << 16),
+                                      snap4(x2, s2) | (((uint32_t)cell | ((m ^ d) << 7)) << 16));
         if (b.depth < kLds4Levels) s_stk[b.depth][HI][w.lane] = snap;
         else g_stk[(b.depth * 2 + HI) * 64 + w.lane] = snap;
-        if (w.hl == 0) br[b.depth] = (uint32_t)cell | ((m ^ d) << 16);
         ++b.depth;
         b.maxd = max(b.maxd, b.depth);
         set_cell4<HI>(w, c, cell, d);
@@ -490,32 +541,37 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
         finish_board4<HI>(w, a, b, c, b.count > 0 ? 1 : 0);
         return;
     }
-    const uint32_t rec = br[b.depth - 1];
-    const int cell = (int)(rec & 0xFFu);
-    uint32_t rest = rec >> 16;
+    const uint32_t lvl = b.depth - 1;
+    const uint2 snap = lvl < kLds4Levels ? s_stk[lvl][HI][w.lane] : g_stk[(lvl * 2 + HI) * 64 + w.lane];
+    const uint32_t rec = snap.y >> 16;
+    const int cell = (int)(rec & 0x7Fu);
+    uint32_t rest = rec >> 7;
     const uint32_t d = rest & (0u - rest);
     rest ^= d;
-    const uint2 snap =
-        b.depth - 1 < kLds4Levels ? s_stk[b.depth - 1][HI][w.lane] : g_stk[((b.depth - 1) * 2 + HI) * 64 + w.lane];
-    const uint32_t y0 = snap.x & 0xFFFFu, y1 = snap.x >> 16, y2 = snap.y;
+    const uint32_t y0 = snap.x & 0xFFFFu, y1 = snap.x >> 16, y2 = snap.y & 0xFFFFu;
     c.x0 = setfld<HI>(c.x0, snap_x4(y0));
     c.x1 = setfld<HI>(c.x1, snap_x4(y1));
     c.x2 = setfld<HI>(c.x2, snap_x4(y2));
     c.s0 = setfld<HI>(c.s0, snap_s4(y0));
     c.s1 = setfld<HI>(c.s1, snap_s4(y1));
     c.s2 = setfld<HI>(c.s2, snap_s4(y2));
-    if (rest == 0) --b.depth;
-    else if (w.hl == 0) br[b.depth - 1] = (uint32_t)cell | (rest << 16);
+    if (rest == 0) {
+        --b.depth;
+    } else {
+        const uint32_t y = y2 | (((uint32_t)cell | (rest << 7)) << 16);
+        if (lvl < kLds4Levels) s_stk[lvl][HI][w.lane].y = y;
+        else g_stk[(lvl * 2 + HI) * 64 + w.lane].y = y;
+    }
     set_cell4<HI>(w, c, cell, d);
 }
 
 // step of slot HI: its state comes from and returns to LDS; returns whether the slot is active
 template <int HI>
-__device__ __forceinline__ bool step4(const Lane4& w, const Args4& a, Cells4& c, bool bad, uint32_t* s_br,
+__device__ __forceinline__ bool step4(const Lane4& w, const Args4& a, Cells4& c, bool bad,
                                       uint2 (*s_stk)[2][64], uint2* g_stk, Slot4* s_slot) {
     Slot4* p = s_slot + w.half * 2 + HI;
     Slot4 b = *p;
-    step4_body<HI>(w, a, b, c, bad, s_br, s_stk, g_stk);
+    step4_body<HI>(w, a, b, c, bad, s_stk, g_stk);
     if (w.hl == 0) *p = b;
     return b.active != 0u;
 }
@@ -535,14 +591,12 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
 
 #ifdef SDK_DEFINE_SOLVE4_KERNEL   // defined in solve4_launch.hip only
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {
-    __shared__ uint2 s_cell[2 * kCells4];
-    __shared__ uint2 s_unit[2 * 32];
+    __shared__ uint2 s_region[2 * kRegion4];
     __shared__ uint8_t s_in[2 * 2 * 81];
-    __shared__ uint32_t s_br[2 * 2 * kMaxDepth];
-    __shared__ uint2 s_stk[kLds4Levels][2][64];
+    __shared__ uint2 s_stk[kLds4Levels > 0 ? kLds4Levels : 1][2][64];   // unused when kLds4Levels = 0
     __shared__ Slot4 s_slot[4];
     Lane4 w;
-    init_lane4(w, s_cell, s_unit, s_in);
+    init_lane4(w, s_region, s_in);
     uint2* g_stk = reinterpret_cast<uint2*>(args.stack) + (size_t)blockIdx.x * (kMaxDepth * 2 * 64);
     Args4 a;
     a.in = args.in;
@@ -586,13 +640,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
         if (E0 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E0))
-                r = step4<0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_br, s_stk, g_stk, s_slot);
+                r = step4<0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot);
             A0 = (A0 & ~E0) | (__builtin_amdgcn_ballot_w64(r) & E0);
         }
         if (E1 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E1))
-                r = step4<1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_br, s_stk, g_stk, s_slot);
+                r = step4<1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot);
             A1 = (A1 & ~E1) | (__builtin_amdgcn_ballot_w64(r) & E1);
         }
     }

@@ -124,10 +124,16 @@ __device__ __forceinline__ bool half_any_s(bool pred) {
     return __builtin_amdgcn_inverse_ballot_w64(lo | hi);
 }
 
-// min over the 32 lanes of each half (all lanes of the half must be active)
+// min over the 32 lanes of each half (all lanes of the half must be active).
+// ds_swizzle in bitmask mode (xor_mask << 10 | and_mask 0x1F) exchanges within 32
+// lanes with no address register (a __shfl_xor's lane addresses are loop-invariant,
+// so the compiler hoists and, under register pressure, spills them).
 __device__ __forceinline__ uint32_t half_min(uint32_t v) {
-#pragma unroll
-    for (int m = 1; m < 32; m <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m));
+    v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (1 << 10) | 0x1F));
+    v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (2 << 10) | 0x1F));
+    v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1F));
+    v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (8 << 10) | 0x1F));
+    v = min(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (16 << 10) | 0x1F));
     return v;
 }
 

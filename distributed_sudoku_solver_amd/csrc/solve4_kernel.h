@@ -64,6 +64,33 @@ namespace sdk {
 // 2 levels / 6 waves 692M/s, 0 / 7 731M/s, 0 / 8 715M/s, the last spilling outside
 // the round).
 constexpr int kLds4Levels = SDK_SOLVE4_LDS_LEVELS;
+
+// Profiling build only (tools/build_variant.sh prof -DSDK_SOLVE4_PROFILE=1,
+// tools/solve4_prof.py): shader-clock cycles of the wave per part of the loop, summed
+// over all waves into g_prof4 (0 rounds, 1/2 steps of slot 0/1, 3 finish + next board,
+// 4 locked candidates, 5 backtrack, 6 branch, 8 whole loop, 9 loop iterations).
+#ifndef SDK_SOLVE4_PROFILE
+#define SDK_SOLVE4_PROFILE 0
+#endif
+#if SDK_SOLVE4_PROFILE
+__device__ unsigned long long g_prof4[10];
+__shared__ unsigned long long s_prof4[10];   // this wave's sums (one wave per workgroup)
+__device__ __forceinline__ void prof4_add(int k, uint64_t v) {
+    const uint64_t em = __builtin_amdgcn_read_exec();
+    if ((int)__lane_id() == __builtin_ctzll(em)) s_prof4[k] += v;
+}
+#define PROF4(k, ...)                                               \
+    do {                                                            \
+        const uint64_t t0_ = __builtin_amdgcn_s_memtime();          \
+        __VA_ARGS__;                                                \
+        prof4_add(k, __builtin_amdgcn_s_memtime() - t0_);           \
+    } while (0)
+#else
+#define PROF4(k, ...) \
+    do {              \
+        __VA_ARGS__;  \
+    } while (0)
+#endif
 constexpr int kStack4WordsPerBlock = kMaxDepth * 2 * 64 * 2;
 constexpr uint32_t kC2 = 0x01FF01FFu;                 // candidate bits of both boards
 constexpr uint32_t kInert4 = 0x200u;                  // inert marker (one board)
@@ -132,23 +159,42 @@ struct Lane4 {
     uint8_t* s_in;            // this half's input bytes, [slot][81]
 };
 
-__device__ __forceinline__ void init_lane4(Lane4& w, uint2* s_region_all, uint8_t* s_in_all) {
-    Lane2 l2;
-    init_lane2(l2, nullptr, nullptr);
-    w.lane = l2.lane;
-    w.hl = l2.hl;
-    w.half = l2.half;
-    w.act = l2.act;
+// per-lane fields from a lane id (everything but ucell)
+__device__ __forceinline__ void lane4_base(Lane4& w, uint2* s_region_all, uint8_t* s_in_all, int lane) {
+    w.lane = lane;
+    w.hl = lane & 31;
+    w.half = lane >> 5;
+    w.act = w.hl < 27;
     const int j = w.act ? w.hl : 0;
     w.c0 = w.act ? j : 91 + (w.hl - 27);
     w.ucol = 9 + j % 9;
     w.ur0 = j / 9;
     w.ub0 = 18 + (j % 9) / 3;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) w.ucell[k] = l2.ucell[k];
     w.s_cell = s_region_all + w.half * kRegion4;
     w.s_unit = w.s_cell + kCells4;
     w.s_in = s_in_all + w.half * 2 * 81;
+}
+
+// the propagation loop's lane (all fields)
+__device__ __forceinline__ void init_lane4(Lane4& w, uint2* s_region_all, uint8_t* s_in_all) {
+    Lane2 l2;
+    init_lane2(l2, nullptr, nullptr);
+    lane4_base(w, s_region_all, s_in_all, (int)threadIdx.x);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w.ucell[k] = l2.ucell[k];
+}
+
+// The search steps' lane: the same fields (ucell aside) from a lane id that a volatile
+// asm reads, so the compiler cannot hoist what the steps derive from it out of the
+// propagation loop.  Hoisted and kept live across the loop, those addresses and
+// indices spilled to scratch and every step waited on memory to reload them; the
+// round's own LDS addresses (the loop lane's) stay in registers.
+__device__ __forceinline__ Lane4 lane4_fresh(uint2* s_region_all, uint8_t* s_in_all) {
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    Lane4 w;
+    lane4_base(w, s_region_all, s_in_all, lane);
+    return w;
 }
 
 __device__ __forceinline__ bool half_any4(const Lane4& w, bool pred) {
@@ -157,7 +203,8 @@ __device__ __forceinline__ bool half_any4(const Lane4& w, bool pred) {
 }
 
 __device__ __forceinline__ uint32_t half_first4(const Lane4& w, uint32_t v) {
-    return (uint32_t)__shfl((int)v, w.half * 32);
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 32);
+    return w.half ? b : a;
 }
 
 // a wave-uniform 64-bit lane mask with every 32-lane half that has a set bit filled
@@ -349,7 +396,76 @@ __device__ __forceinline__ uint32_t snap_s4(uint32_t y) {
 // kernel arguments as plain values plus the wave's propagation-loop iteration
 struct Args4 : Args2 {
     uint32_t iter;
+    int locked;
 };
+
+// Locked candidates (pointing and claiming) for the board in slot HI, run at its
+// propagation fixpoints before it branches (SDK_OPT_LOCKED).  Over the 54 box-line
+// intersections ("triads": row r x stack s, column c x band b, three cells each):
+//   pointing  the digits of a box confined to one of its triads leave the rest of
+//             that triad's line;
+//   claiming  the digits of a line confined to one of its triads leave the rest of
+//             that triad's box.
+// Both only remove digits that occur in no completion of the node (every unit of
+// the board exact: each digit exactly once per unit), so the set of completions,
+// and with it the lex-first one the reference returns, is unchanged; only the
+// search takes fewer nodes (tools/round_model.py: the five 17-clue classes need no
+// branch at all, 1.78 -> 1.00 nodes per puzzle).  Boards with a unit that is not
+// exact (duplicated or inert givens) skip the rule.
+// Layout: triad t = 3 * line + (index of the crossing box along the line), so the 9
+// triads of a band (rows) or stack (columns) are t = 9g .. 9g + 8 and "row k of box s'"
+// of that group is t = 9g + 3k + s'.  Lane j < 27 owns row triad j and column triad
+// j; phase 1 stores (row OR, column OR) of X at s_unit[kTri4 + t], phase 2 reads the
+// 8 other triads of its group in an order rotated to put its own first and stores
+// the eliminations of its two triads at s_unit[kElim4 + t], phase 3 applies them to
+// the lane's cells (cell (R, C): row triad 3R + C/3, column triad 3C + R/3).
+// Returns whether a candidate of slot HI was removed (uniform in the half).
+constexpr int kTri4 = 32, kElim4 = 59;                // scratch slots in the unit region
+template <int HI>
+__device__ __forceinline__ bool lc4(const Lane4& w, Cells4& c) {
+    if (half_any4(w, w.act && fld<HI>(c.E) == 0u)) return false;
+    w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
+    w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
+    w.s_cell[w.c0 + 54] = make_uint2(c.x2, c.s2);
+    __syncthreads();
+    const int j = w.hl;
+    if (w.act) {
+        const int rb = (j / 3) * 9 + 3 * (j % 3), cb = 27 * (j % 3) + j / 3;
+        const uint32_t rt = w.s_cell[rb].x | w.s_cell[rb + 1].x | w.s_cell[rb + 2].x;
+        const uint32_t ct = w.s_cell[cb].x | w.s_cell[cb + 9].x | w.s_cell[cb + 18].x;
+        w.s_unit[kTri4 + j] = make_uint2(rt, ct);
+    }
+    __syncthreads();
+    if (w.act) {
+        const int g = 9 * (j / 9), k0 = (j % 9) / 3, s0 = j % 3;
+        const int r0 = g + 3 * k0, ra = g + 3 * ((k0 + 1) % 3), rb = g + 3 * ((k0 + 2) % 3);
+        const int c1 = (s0 + 1) % 3, c2 = (s0 + 2) % 3;
+        const uint2* t = w.s_unit + kTri4;
+        const uint2 a01 = t[r0 + c1], a02 = t[r0 + c2];
+        const uint2 a10 = t[ra + s0], a11 = t[ra + c1], a12 = t[ra + c2];
+        const uint2 a20 = t[rb + s0], a21 = t[rb + c1], a22 = t[rb + c2];
+        // pointing from the two other boxes of the line | claiming by the two other lines of the box
+        const uint32_t er = (a01.x & ~(a11.x | a21.x)) | (a02.x & ~(a12.x | a22.x)) | (a10.x & ~(a11.x | a12.x)) |
+                            (a20.x & ~(a21.x | a22.x));
+        const uint32_t ec = (a01.y & ~(a11.y | a21.y)) | (a02.y & ~(a12.y | a22.y)) | (a10.y & ~(a11.y | a12.y)) |
+                            (a20.y & ~(a21.y | a22.y));
+        w.s_unit[kElim4 + j] = make_uint2(er, ec);
+    }
+    __syncthreads();
+    bool ch = false;
+    if (w.act) {
+        const uint32_t fm = HI ? 0x01FF0000u : 0x1FFu;
+        const int rt0 = (j / 9) * 3 + (j % 9) / 3, ct0 = (j % 9) * 3;
+        const uint2* e = w.s_unit + kElim4;
+        const uint32_t e0 = (e[rt0].x | e[ct0].y) & fm, e1 = (e[rt0 + 9].x | e[ct0 + 1].y) & fm,
+                       e2 = (e[rt0 + 18].x | e[ct0 + 2].y) & fm;
+        ch = ((c.x0 & e0) | (c.x1 & e1) | (c.x2 & e2)) != 0u;
+        c.x0 &= ~e0;
+        c.x1 &= ~e1;
+        c.x2 &= ~e2;
+    }
+    return half_any4(w, ch);
+}
 
 template <int HI>
 __device__ __forceinline__ void start_board4(const Lane4& w, const Args4& a, Slot4& b, Cells4& c, bool reload) {
@@ -417,7 +533,7 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
 }
 
 template <int HI>
-__device__ __forceinline__ void next_board4(const Lane4& w, const Args4& a, Slot4& b, Cells4& c) {
+__device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c) {
     ++b.bidx;
     if (b.bidx >= b.bend) {
         uint32_t base = 0;
@@ -442,11 +558,12 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Args4& a, Slot
         c.s1 = setfld<HI>(c.s1, kInert4);
         c.s2 = setfld<HI>(c.s2, kInert4);
     }
-    statics4<HI>(w, c);
+    statics4<HI>(wr, c);   // the loop lane's LDS addresses: the round's, live anyway
 }
 
 template <int HI>
-__device__ __forceinline__ void finish_board4(const Lane4& w, const Args4& a, Slot4& b, Cells4& c, int st) {
+__device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c,
+                                              int st) {
     uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
     if (st != 1 && w.act) {           // the reference restores the grid (DHT_Node.py:535)
         const uint8_t* sin = w.s_in + HI * 81;
@@ -460,7 +577,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Args4& a, Sl
             a.work[b.bidx] = a.work_rounds == 1 ? (uint64_t)(a.iter - b.rstart)
                                                 : (a.work_rounds == 2 ? (uint64_t)b.maxd : b.nodes);
     }
-    next_board4<HI>(w, a, b, c);
+    next_board4<HI>(w, wr, a, b, c);
 }
 
 __device__ __forceinline__ uint32_t branch_key4(uint32_t x, uint32_t s, int cell, int order) {
@@ -520,7 +637,7 @@ __device__ __forceinline__ void set_cell4(const Lane4& w, Cells4& c, int cell, u
 // digits << 7, uniform in the half -- in the free upper 16 bits of its own snapshot
 // word y, so a level is one 8-byte word per lane and needs no shared record array.
 template <int HI>
-__device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4& b, Cells4& c, bool bad,
+__device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c, bool bad,
                                            uint2 (*s_stk)[2][64], uint2* g_stk) {
     ++b.nodes;
     const uint32_t x0 = fld<HI>(c.x0), x1 = fld<HI>(c.x1), x2 = fld<HI>(c.x2);
@@ -528,7 +645,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
     int r = bad ? P_CONTRA
                 : (half_any4(w, w.act && (x0 | x1 | x2) != 0u) ? P_OPEN : P_SOLVED);
     if (a.budget && b.nodes > a.budget) {
-        finish_board4<HI>(w, a, b, c, -2);
+        PROF4(3, finish_board4<HI>(w, wr, a, b, c, -2));
         return;
     }
     if (r == P_SOLVED) {
@@ -547,13 +664,22 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
                 b.lim = 1;
                 start_board4<HI>(w, a, b, c, false);
             } else {
-                finish_board4<HI>(w, a, b, c, 1);
+                PROF4(3, finish_board4<HI>(w, wr, a, b, c, 1));
             }
             return;
         }
         r = P_CONTRA;
     }
     if (r == P_OPEN) {
+        bool lc = false;
+        if (a.locked == 2 || (a.locked == 1 && b.depth == 0)) PROF4(4, lc = lc4<HI>(w, c));
+        if (lc) {                           // candidates removed: same node, propagate again
+            --b.nodes;
+            return;
+        }
+#if SDK_SOLVE4_PROFILE
+        const uint64_t tb_ = __builtin_amdgcn_s_memtime();
+#endif
         int cell;
         uint32_t m;
         if (b.order == ORDER_LEX) {
@@ -575,13 +701,19 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
         ++b.depth;
         b.maxd = max(b.maxd, b.depth);
         set_cell4<HI>(w, c, cell, d);
+#if SDK_SOLVE4_PROFILE
+        prof4_add(6, __builtin_amdgcn_s_memtime() - tb_);
+#endif
         return;
     }
     // contradiction: resume the deepest level with untried digits
     if (b.depth == 0) {
-        finish_board4<HI>(w, a, b, c, b.count > 0 ? 1 : 0);
+        PROF4(3, finish_board4<HI>(w, wr, a, b, c, b.count > 0 ? 1 : 0));
         return;
     }
+#if SDK_SOLVE4_PROFILE
+    const uint64_t tk_ = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t lvl = b.depth - 1;
     const uint2 snap = lvl < kLds4Levels ? s_stk[lvl][HI][w.lane] : g_stk[(lvl * 2 + HI) * 64 + w.lane];
     const uint32_t rec = snap.y >> 16;
@@ -604,16 +736,20 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Args4& a, Slot4
         else g_stk[(lvl * 2 + HI) * 64 + w.lane].y = y;
     }
     set_cell4<HI>(w, c, cell, d);
+#if SDK_SOLVE4_PROFILE
+    prof4_add(5, __builtin_amdgcn_s_memtime() - tk_);
+#endif
 }
 
 // step of slot HI: its state comes from and returns to LDS; returns whether the slot is active
 template <int HI>
-__device__ __forceinline__ bool step4(const Lane4& w, const Args4& a, Cells4& c, bool bad,
-                                      uint2 (*s_stk)[2][64], uint2* g_stk, Slot4* s_slot) {
+__device__ __forceinline__ bool step4(const Lane4& wr, const Args4& a, Cells4& c, bool bad, uint2 (*s_stk)[2][64],
+                                      uint2* g_stk_all, Slot4* s_slot, uint2* s_region, uint8_t* s_in) {
+    const Lane4 w = lane4_fresh(s_region, s_in);
+    uint2* g_stk = g_stk_all + (size_t)blockIdx.x * (kMaxDepth * 2 * 64);
     Slot4* p = s_slot + w.half * 2 + HI;
-    Slot4 b = *p;
-    step4_body<HI>(w, a, b, c, bad, s_stk, g_stk);
-    if (w.hl == 0) *p = b;
+    Slot4 b;
+    PROF4(1 + HI, b = *p; step4_body<HI>(w, wr, a, b, c, bad, s_stk, g_stk); if (w.hl == 0) *p = b);
     return b.active != 0u;
 }
 
@@ -625,7 +761,7 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
     b.bend = 0;
     b.depth = 0;
     b.count = 0;
-    next_board4<HI>(w, a, b, c);
+    next_board4<HI>(w, w, a, b, c);
     if (w.hl == 0) s_slot[w.half * 2 + HI] = b;
     return b.active != 0u;
 }
@@ -638,7 +774,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     __shared__ Slot4 s_slot[4];
     Lane4 w;
     init_lane4(w, s_region, s_in);
-    uint2* g_stk = reinterpret_cast<uint2*>(args.stack) + (size_t)blockIdx.x * (kMaxDepth * 2 * 64);
+#if SDK_SOLVE4_PROFILE
+    if (threadIdx.x < 10) s_prof4[threadIdx.x] = 0;
+    __syncthreads();
+#endif
+    uint2* g_stk = reinterpret_cast<uint2*>(args.stack);   // the steps add this workgroup's offset
     Args4 a;
     a.in = args.in;
     a.in_first = args.in_first;
@@ -654,6 +794,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     a.work_rounds = args.work_rounds;
     a.budget = args.budget;
     a.iter = 0;
+    a.locked = args.locked;
 
     Cells4 c;
     c.x0 = c.x1 = c.x2 = 0u;
@@ -668,9 +809,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     // when it contradicted (B) or nothing changed (no C) in its half.  A* = halves
     // whose slot still has a board.
     uint64_t A0 = __builtin_amdgcn_ballot_w64(act0), A1 = __builtin_amdgcn_ballot_w64(act1);
+#if SDK_SOLVE4_PROFILE
+    const uint64_t tl_ = __builtin_amdgcn_s_memtime();
+#endif
     while ((A0 | A1) != 0) {
         uint32_t bm, zmin, chg;
-        round4(w, c, bm, zmin, chg);
+        PROF4(0, round4(w, c, bm, zmin, chg));
         ++a.iter;
         const uint32_t badw = bm | z16(zmin);
         const uint64_t B0 = spread_halves(__builtin_amdgcn_ballot_w64((badw & 0xFFFFu) != 0u));
@@ -681,16 +825,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
         if (E0 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E0))
-                r = step4<0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot);
+                r = step4<0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot, s_region, s_in);
             A0 = (A0 & ~E0) | (__builtin_amdgcn_ballot_w64(r) & E0);
         }
         if (E1 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E1))
-                r = step4<1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot);
+                r = step4<1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot, s_region, s_in);
             A1 = (A1 & ~E1) | (__builtin_amdgcn_ballot_w64(r) & E1);
         }
     }
+#if SDK_SOLVE4_PROFILE
+    prof4_add(8, __builtin_amdgcn_s_memtime() - tl_);
+    prof4_add(9, a.iter);
+    __syncthreads();
+    if (threadIdx.x < 10) atomicAdd(&g_prof4[threadIdx.x], s_prof4[threadIdx.x]);
+#endif
 }
 #endif  // SDK_DEFINE_SOLVE4_KERNEL
 

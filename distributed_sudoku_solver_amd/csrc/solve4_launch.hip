@@ -13,3 +13,15 @@ hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream) 
 }
 
 }  // namespace sdk
+
+#if SDK_SOLVE4_PROFILE
+// profiling build only: the g_prof4 counters (see solve4_kernel.h), optionally zeroed
+extern "C" int sdk_debug_prof4(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sdk::g_prof4), sizeof(sdk::g_prof4)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long zero[10] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(sdk::g_prof4), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

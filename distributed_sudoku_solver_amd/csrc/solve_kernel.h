@@ -76,6 +76,7 @@ struct SolveArgs {
     int work_rounds;           // what work[] counts: 0 search nodes, 1 propagation rounds, 2 max DFS depth
     uint64_t in_first;         // board i of the launch reads in[(in_first + i*in_step)*81];
     uint64_t in_step;          // outputs stay dense (out[i*81], status[i]); 0/1 = contiguous
+    int locked;                // QUAD solver: locked-candidates pass at fixpoints (SDK_OPT_LOCKED)
 };
 
 __device__ __forceinline__ uint32_t cell_init(uint32_t v) {

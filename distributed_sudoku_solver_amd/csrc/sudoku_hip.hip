@@ -72,6 +72,7 @@ struct sdk_ctx {
     int solve_chunk = 0;          // boards per dequeue, 0 = automatic
     int work_rounds = 0;
     int solver = SDK_SOLVER_QUAD;
+    int locked = 1;                // QUAD: locked candidates at fixpoints (fewer search nodes, same answers)
     int waves_per_cu2 = 32;       // solve2/solve4 grid per CU (24 resident: 80 VGPRs, <= 6.8 KB LDS; the rest
                                   // start as the first retire, and the smaller dequeue chunk trims the tail)
     // workspaces
@@ -198,6 +199,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.work_rounds = c->work_rounds;
     a.in_first = in_first;
     a.in_step = in_step;
+    a.locked = c->locked;
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
     if (rc) return rc;
@@ -468,6 +470,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 0 || value > 4096) return fail(SDK_EINVAL, "solve chunk must be 0..4096");
             c->solve_chunk = (int)value;
             return SDK_OK;
+        case SDK_OPT_LOCKED:
+            if (value < 0 || value > 2) return fail(SDK_EINVAL, "locked must be 0, 1 or 2");
+            c->locked = (int)value;
+            return SDK_OK;
         case SDK_OPT_CHECK_VARIANT:
             if (value < SDK_CHECK_REG1 || value > SDK_CHECK_GLDS4) return fail(SDK_EINVAL, "bad check variant %lld", (long long)value);
             c->check_variant = (int)value;
@@ -492,6 +498,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_CHECK_VARIANT: *value = c->check_variant; return SDK_OK;
         case SDK_OPT_SOLVE_CHUNK: *value = c->solve_chunk; return SDK_OK;
         case SDK_OPT_TIMING: *value = c->timing ? 1 : 0; return SDK_OK;
+        case SDK_OPT_LOCKED: *value = c->locked; return SDK_OK;
         case SDK_OPT_TIMER_EVENTS: *value = (int64_t)c->events.size(); return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }

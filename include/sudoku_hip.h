@@ -75,6 +75,10 @@ extern "C" {
 #define SDK_OPT_TIMING       11  /* 1 = bracket every kernel with HIP events for        */
                                  /* sdk_timer_read (default 0: no events are created)    */
 #define SDK_OPT_TIMER_EVENTS 12  /* read-only: HIP event pairs the context holds         */
+#define SDK_OPT_LOCKED       13  /* QUAD solver: locked-candidates pass (pointing /      */
+                                 /* claiming) at propagation fixpoints before branching: */
+                                 /* 0 never, 1 at the root node only (default), 2 at     */
+                                 /* every node; same answers, fewer search nodes         */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

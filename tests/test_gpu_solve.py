@@ -310,18 +310,23 @@ def test_ragged_batch_sizes(solver_engine, n):
 
 
 def test_solvers_take_identical_search_paths(engine):
-    """Same propagation, same branching: per-board search nodes and propagation rounds agree."""
+    """Same propagation, same branching: per-board search nodes and propagation rounds agree
+    (QUAD with its locked-candidates pass off: the other solvers have no such rule)."""
     p, _ = synth.make_17clue(3000, seed=7)
     sparse = _random_puzzles(300, 8, 18, 28)
     boards = np.concatenate([p, sparse])
     res = {}
-    for solver in SOLVERS:
-        engine.set_option(L.SDK_OPT_SOLVER, solver)
-        for kind in (L.SDK_WORK_NODES, L.SDK_WORK_ROUNDS):
-            engine.set_option(L.SDK_OPT_WORK_COUNTER, kind)
-            res[(solver, kind)] = engine.solve_batch(boards, want_work=True)
-    engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
-    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
+    engine.set_option(L.SDK_OPT_LOCKED, 0)
+    try:
+        for solver in SOLVERS:
+            engine.set_option(L.SDK_OPT_SOLVER, solver)
+            for kind in (L.SDK_WORK_NODES, L.SDK_WORK_ROUNDS):
+                engine.set_option(L.SDK_OPT_WORK_COUNTER, kind)
+                res[(solver, kind)] = engine.solve_batch(boards, want_work=True)
+    finally:
+        engine.set_option(L.SDK_OPT_LOCKED, 1)
+        engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
+        engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
     for kind in (L.SDK_WORK_NODES, L.SDK_WORK_ROUNDS):
         a = res[(SOLVERS[0], kind)]
         for other in SOLVERS[1:]:
@@ -440,3 +445,44 @@ def test_frontier_1m_boards_multiworkgroup_scan(engine):
     out, st = sharded_solve(engine, synth.parse(DEMO), 0, 1, target=300_000)
     assert st == 1 and "".join(map(str, out)) == \
         "234156789179328456568479132391245678425687391687913245752831964816794523943562817"
+
+
+@pytest.mark.parametrize("order", ORDERS, ids=["mrv_unique", "lex"])
+def test_locked_candidates_same_answers_fewer_nodes(engine, order):
+    """QUAD's locked-candidates pass (SDK_OPT_LOCKED) removes only digits that are in no
+    completion: every board, status and lex-first answer is the one without it, on unique,
+    multi-solution, conflicting and out-of-domain boards; the transformed 17-clue classes
+    need no branch at all, and minimal puzzles take fewer search nodes."""
+    p17, s17 = synth.make_17clue(20000, seed=5)
+    pmin, smin = synth.make_minimal(20000, threads=16)
+    sparse = _random_puzzles(1000, 44, 12, 30)
+    odd = _random_puzzles(600, 45, 20, 45)
+    rng = np.random.default_rng(46)
+    for i in range(len(odd)):
+        nz = np.flatnonzero(odd[i])
+        if i % 2 == 0 and len(nz) >= 2:
+            a, b = rng.choice(nz, 2, replace=False)
+            odd[i, b] = odd[i, a]
+        else:
+            odd[i, rng.choice(81, 2, replace=False)] = rng.integers(10, 256, 2)
+    boards = np.concatenate([p17, pmin, sparse, odd])
+    n17, nmin = len(p17), len(pmin)
+    res = {}
+    engine.set_option(L.SDK_OPT_ORDER, order)
+    engine.set_option(L.SDK_OPT_NODE_BUDGET, 200_000)
+    try:
+        for lc in (1, 0):
+            engine.set_option(L.SDK_OPT_LOCKED, lc)
+            res[lc] = engine.solve_batch(boards, want_work=True)
+    finally:
+        engine.set_option(L.SDK_OPT_LOCKED, 1)
+        engine.set_option(L.SDK_OPT_NODE_BUDGET, 0)
+        engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
+    (o1, st1, w1), (o0, st0, w0) = res[1], res[0]
+    assert (st1[:n17 + nmin] == 1).all()
+    assert (o1[:n17] == s17).all() and (o1[n17:n17 + nmin] == smin).all()
+    done = (st1 != -2) & (st0 != -2)
+    assert done.mean() > 0.95
+    assert (st1[done] == st0[done]).all() and (o1[done] == o0[done]).all()
+    assert (w1[:n17] == 1).all(), np.bincount(w1[:n17].astype(np.int64))
+    assert w1[n17:n17 + nmin].mean() < w0[n17:n17 + nmin].mean()

@@ -21,6 +21,7 @@ ap.add_argument("--waves-per-cu", type=int, default=0)
 ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave", "quad"])
 ap.add_argument("--sweep", action="store_true", help="time waves-per-CU settings")
 ap.add_argument("--order", default="lex", choices=["mrv_unique", "lex"])
+ap.add_argument("--locked", type=int, default=1, help="QUAD: locked-candidates pass (SDK_OPT_LOCKED: 0 off, 1 root, 2 all nodes)")
 args = ap.parse_args()
 
 if args.workload == "minimal":
@@ -30,6 +31,7 @@ else:
     p, s = gen(args.n, seed=11)
 with SudokuEngine(0) as eng:
     eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
+    eng.set_option(L.SDK_OPT_LOCKED, args.locked)
     eng.set_option(L.SDK_OPT_SOLVER, {"halfwave": L.SDK_SOLVER_HALFWAVE, "wave": L.SDK_SOLVER_WAVE,
                                       "quad": L.SDK_SOLVER_QUAD}[args.solver])
     wopt = L.SDK_OPT_WAVES_PER_CU if args.solver == "wave" else L.SDK_OPT_WAVES_PER_CU2
@@ -46,7 +48,7 @@ with SudokuEngine(0) as eng:
     ms, nl = eng.timer_read()
     out = np.empty((args.n, 81), np.uint8)
     d_out.download(out)
-    print(f"{args.solver} {args.order} {args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
+    print(f"{args.solver} {args.order} lc={args.locked} {args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
           f"ok={(out == s).all()}", flush=True)
     if args.sweep:
         for wpc in (8, 12, 16, 20, 24, 32):

@@ -302,6 +302,14 @@ __device__ __forceinline__ void unit4(const uint2 (&v)[9], uint32_t E, uint32_t 
 #define SDK_SOLVE4_SPLIT_READS 1
 #endif
 
+// Ordering point between LDS phases of the one-wave workgroup.  A wave's LDS
+// instructions execute in issue order, so a read after a store sees it and a store
+// after a read cannot overtake it; all that is needed is that the compiler keeps
+// the program order of the accesses (may-alias LDS accesses are never reordered
+// across a wave barrier).  __syncthreads() adds s_waitcnt lgkmcnt(0) before every
+// phase (and would also drain the VM counter, see DESIGN.md on LDS-DMA prefetch).
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
 // LDS byte address of a __shared__ object (for inline-asm ds_* operands)
 __device__ __forceinline__ uint32_t lds_addr4(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
@@ -313,14 +321,14 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
     w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
     w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
     w.s_cell[w.c0 + 54] = make_uint2(c.x2, c.s2);
-    __syncthreads();
+    wave_sync();
     uint2 v[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) v[k] = w.s_cell[w.ucell[k]];
     uint32_t once, T;
     unit4(v, c.E, c.D, once, T, bm);
     w.s_unit[w.c0] = make_uint2(T, once);
-    __syncthreads();
+    wave_sync();
     uint32_t m0, m1, m2;
     chg = 0;
 #if SDK_SOLVE4_SPLIT_READS
@@ -424,10 +432,9 @@ constexpr int kTri4 = 32, kElim4 = 59;                // scratch slots in the un
 template <int HI>
 __device__ __forceinline__ bool lc4(const Lane4& w, Cells4& c) {
     if (half_any4(w, w.act && fld<HI>(c.E) == 0u)) return false;
-    w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
-    w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
-    w.s_cell[w.c0 + 54] = make_uint2(c.x2, c.s2);
-    __syncthreads();
+    // The cell words in LDS are this board's current ones: its last round stored them and
+    // changed nothing (a fixpoint), and nothing but a round or statics4 -- which stores
+    // the registers -- writes them in between.
     const int j = w.hl;
     if (w.act) {
         const int rb = (j / 3) * 9 + 3 * (j % 3), cb = 27 * (j % 3) + j / 3;
@@ -435,7 +442,7 @@ __device__ __forceinline__ bool lc4(const Lane4& w, Cells4& c) {
         const uint32_t ct = w.s_cell[cb].x | w.s_cell[cb + 9].x | w.s_cell[cb + 18].x;
         w.s_unit[kTri4 + j] = make_uint2(rt, ct);
     }
-    __syncthreads();
+    wave_sync();
     if (w.act) {
         const int g = 9 * (j / 9), k0 = (j % 9) / 3, s0 = j % 3;
         const int r0 = g + 3 * k0, ra = g + 3 * ((k0 + 1) % 3), rb = g + 3 * ((k0 + 2) % 3);
@@ -451,7 +458,7 @@ __device__ __forceinline__ bool lc4(const Lane4& w, Cells4& c) {
                             (a20.y & ~(a21.y | a22.y));
         w.s_unit[kElim4 + j] = make_uint2(er, ec);
     }
-    __syncthreads();
+    wave_sync();
     bool ch = false;
     if (w.act) {
         const uint32_t fm = HI ? 0x01FF0000u : 0x1FFu;
@@ -517,7 +524,7 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
     w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
     w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
     w.s_cell[w.c0 + 54] = make_uint2(c.x2, c.s2);
-    __syncthreads();
+    wave_sync();
     uint32_t os = 0, ts = 0;
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
@@ -525,7 +532,7 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
         ts |= os & v;
         os |= v;
     }
-    __syncthreads();   // the next round's stores must not overtake these reads
+    wave_sync();   // the next round's stores must not overtake these reads
     const uint32_t dup = ts & kCands;
     const uint32_t exact = (dup == 0u && (os & kInert4) == 0u) ? kCands : 0u;
     c.D = setfld<HI>(c.D, kCands & ~dup);

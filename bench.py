@@ -78,6 +78,8 @@ def parse_args():
     ap.add_argument("--minimal-puzzles", type=int, default=1 << 20,
                     help="distinct minimal-puzzle leg, puzzles per GPU (0 = skip)")
     ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
+    ap.add_argument("--lane-puzzles", type=int, default=200_000,
+                    help="per-lane reference-DFS leg on a C2 prefix (rank 0, N=1; 0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
                     help="watchdog for the side legs: print what was measured and exit")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02", "pmc_c4.json"),
@@ -341,6 +343,47 @@ def minimal_leg(eng, d, args, synth, L):
                         f"({int((p > 0).sum(1).mean())} clues on average) x seeded symmetries",
             "value": d.world * n * 3 / el, "unit": "puzzles/s", "avg_kernel_ms": k_s * 1000.0,
             "search": stats, "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
+
+
+def lane_dfs_leg(eng, args, synth, L):
+    """North-star part (3) beside the propagating solvers: the reference's own naive DFS, ONE
+    BOARD PER LANE with its stack in LDS (SDK_SOLVER_LANE, csrc/solve_lane_kernel.h), on a
+    prefix of the C2 30-clue stream.  Its work counter is the reference's `validations`, so
+    the leg reports validations/s of the same algorithm on the GPU and on the host cores (the
+    oracle's C port), and checks the counts against the port on a sample."""
+    from oracle import oracle as O
+    n = args.lane_puzzles
+    p, sol = synth.make_30clue(n, seed=args.seed + 31)
+    budget = 50_000_000
+    eng.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_LANE)
+    eng.set_option(L.SDK_OPT_NODE_BUDGET, budget)
+    try:
+        eng.solve_batch(p[:4096])
+        eng.synchronize()
+        t0 = time.perf_counter()
+        out, st, val = eng.solve_batch(p, want_work=True)
+        wall = time.perf_counter() - t0
+    finally:
+        eng.set_option(L.SDK_OPT_NODE_BUDGET, 0)
+        eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
+    m = min(n, 4096)
+    cores = args.cpu_cores or cpu_share()
+    t1 = time.perf_counter()
+    ref_out, ref_st, ref_val = O.naive_solve_batch(p[:m], budget=budget, threads=cores)
+    cwall = time.perf_counter() - t1
+    ok = st == 1
+    return {"workload": f"{n} C2 ~30-clue puzzles, one board per lane: the reference's naive DFS "
+                        "(lowest empty cell, digits ascending), LDS-resident digit stack, host-pointer call",
+            "value": n / wall, "unit": "puzzles/s", "validations_per_s": float(val.sum()) / wall,
+            "validations_per_puzzle": {"mean": float(val.mean()), "p99": float(np.percentile(val, 99)),
+                                       "max": int(val.max())},
+            "budget_hits": int((st == -2).sum()),
+            "parity": {"mismatched_boards": int(((out != sol).any(axis=1) & ok).sum() + (~ok & (st != -2)).sum()),
+                       "checked_boards": n,
+                       "validations_vs_c_port": {"sample": m, "equal": int((val[:m] == ref_val).sum()),
+                                                 "status_equal": int((st[:m] == ref_st).sum())}},
+            "c_port_same_dfs": {"validations_per_s": float(ref_val.sum()) / cwall, "cores": cores,
+                                "puzzles_per_s": m / cwall, "sample": m}}
 
 
 def http_leg(requests):
@@ -620,6 +663,11 @@ def main():
 
     if d.rank == 0 and d.world == 1 and args.http_requests > 0:
         result["post_solve_latency"] = http_leg(args.http_requests)
+
+    # -------------------------------------------- per-lane reference DFS (north star part 3)
+    if d.rank == 0 and d.world == 1 and args.lane_puzzles > 0:
+        result["lane_dfs"] = lane_dfs_leg(eng, args, synth, L)
+        bad_total += result["lane_dfs"]["parity"]["mismatched_boards"]
 
     dog.cancel()
     eng.close()

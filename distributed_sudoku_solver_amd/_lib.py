@@ -46,6 +46,7 @@ SDK_CHECK_GLDS4 = 4
 SDK_SOLVER_WAVE = 0
 SDK_SOLVER_HALFWAVE = 1
 SDK_SOLVER_QUAD = 2
+SDK_SOLVER_LANE = 3
 
 SDK_WORK_NODES = 0
 SDK_WORK_ROUNDS = 1

@@ -21,6 +21,8 @@
 #include "frontier_kernel.h"
 #include "solve2_kernel.h"   // constants only: the kernel lives in solve2_launch.hip
 #include "solve4_kernel.h"   // constants only: the kernel lives in solve4_launch.hip
+#define SDK_DEFINE_LANE_KERNEL
+#include "solve_lane_kernel.h"
 
 namespace sdk {
 hipError_t launch_solve2(const SolveArgs& a, unsigned grid, hipStream_t stream);
@@ -157,6 +159,35 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
                  int order = -1) {
     if (n == 0) return SDK_OK;
     if (n > 0x7FFFFFFFull) return fail(SDK_EINVAL, "at most 2^31-1 boards per call");
+    if (c->solver == SDK_SOLVER_LANE && !count_mode) {
+        // one board per lane: the reference's own DFS (solve_lane_kernel.h); `work` =
+        // the reference's validations, the budget counts validations
+        if (!d_out || !d_status) return fail(SDK_EINVAL, "solve needs out and status buffers");
+        if (order == SDK_ORDER_MRV_UNIQUE || (order < 0 && c->order == SDK_ORDER_MRV_UNIQUE))
+            return fail(SDK_EINVAL, "the LANE solver runs the reference's order only (SDK_ORDER_LEX)");
+        int rc = ensure(c->counter, 256);
+        if (rc) return rc;
+        HIPCALL(hipMemsetAsync(c->counter.p, 0, 8, c->stream));
+        sdk::SolveArgs a{};
+        a.in = d_in;
+        a.mask = d_mask;
+        a.out = d_out;
+        a.status = d_status;
+        a.work = d_work;
+        a.n = n;
+        a.next = static_cast<uint32_t*>(c->counter.p);
+        a.budget = c->budget;
+        a.in_first = in_first;
+        a.in_step = in_step;
+        const uint64_t blocks = (n + sdk::kLaneThreads - 1) / sdk::kLaneThreads;
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c->cus * 6));
+        hipEvent_t stop;
+        rc = timer_begin(c, &stop);
+        if (rc) return rc;
+        sdk::solve_lane_kernel<<<grid, sdk::kLaneThreads, 0, c->stream>>>(a);
+        HIPCALL(hipGetLastError());
+        return timer_end(c, stop);
+    }
     // two (solve2_kernel) or four (solve4_kernel) boards per wave for solves; count mode stays
     // one board per wave
     const int per_wave = count_mode ? 1 : (c->solver == SDK_SOLVER_QUAD ? 4 : (c->solver == SDK_SOLVER_HALFWAVE ? 2 : 1));
@@ -458,7 +489,8 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             c->timing = value != 0;
             return SDK_OK;
         case SDK_OPT_SOLVER:
-            if (value != SDK_SOLVER_WAVE && value != SDK_SOLVER_HALFWAVE && value != SDK_SOLVER_QUAD)
+            if (value != SDK_SOLVER_WAVE && value != SDK_SOLVER_HALFWAVE && value != SDK_SOLVER_QUAD &&
+                value != SDK_SOLVER_LANE)
                 return fail(SDK_EINVAL, "bad solver %lld", (long long)value);
             c->solver = (int)value;
             return SDK_OK;

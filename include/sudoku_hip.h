@@ -90,6 +90,10 @@ extern "C" {
 #define SDK_SOLVER_HALFWAVE  1  /* two boards per wavefront, 27 lanes x 3 cells each   */
 #define SDK_SOLVER_QUAD      2  /* four boards per wavefront: HALFWAVE's layout with two */
                                 /* boards packed in the 16-bit halves of every word      */
+#define SDK_SOLVER_LANE      3  /* one board per lane: the reference's naive DFS itself  */
+                                /* (LDS-resident stack); `work` = the reference's        */
+                                /* validations, SDK_OPT_NODE_BUDGET counts validations;  */
+                                /* SDK_ORDER_LEX only; counts use WAVE                   */
 
 #define SDK_WORK_NODES       0  /* search nodes (propagation fixpoints)                */
 #define SDK_WORK_ROUNDS      1  /* propagation rounds (profiling)                      */

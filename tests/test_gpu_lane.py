@@ -1,0 +1,80 @@
+"""One-board-per-lane solver (SDK_SOLVER_LANE): the reference's own DFS per lane.
+
+Besides the boards and statuses, its `work` is the reference's `validations` counter
+(DHT_Node.py:513,527-531), so the golden fixtures' counts pin it directly, and its
+validation budget must stop exactly where the oracle's does."""
+import numpy as np
+import pytest
+
+from distributed_sudoku_solver_amd import synth, _lib as L
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def lane_engine(engine):
+    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_LANE)
+    yield engine
+    engine.set_option(L.SDK_OPT_NODE_BUDGET, 0)
+    engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
+
+
+def test_golden_boards_and_validations(lane_engine, solve_cases):
+    """Reference boards, statuses AND the reference's validation counts (the 55-clash
+    board the reference never finishes is budgeted: status -2, input restored)."""
+    puz = np.array([c["puzzle"] for c in solve_cases], dtype=np.uint8)
+    masks = np.array([O.range_mask(*c["range"]) for c in solve_cases], dtype=np.uint16)
+    lane_engine.set_option(L.SDK_OPT_NODE_BUDGET, 50_000_000)
+    out, st, work = lane_engine.solve_batch(puz, masks, want_work=True)
+    for i, c in enumerate(solve_cases):
+        assert (st[i] == 1) == c["ok"], c["name"]
+        assert out[i].tolist() == (c["board"] if c["ok"] else c["puzzle"]), c["name"]
+        if "validations" in c and c["validations"] is not None:
+            assert int(work[i]) == c["validations"], c["name"]
+
+
+def test_vs_oracle_with_budget(lane_engine):
+    """30-clue, sparse multi-solution, conflicting and out-of-domain boards, random
+    `range` masks, a validation budget: boards, statuses and counts equal the oracle's."""
+    rng = np.random.default_rng(5)
+    p30, _ = synth.make_30clue(3000, seed=5)
+    _, sol = synth.make_17clue(1000, seed=6)
+    sparse = np.where(rng.random((1000, 81)) < rng.uniform(0.15, 0.4, (1000, 1)), sol, 0).astype(np.uint8)
+    odd = sparse[:400].copy()
+    for i in range(len(odd)):
+        nz = np.flatnonzero(odd[i])
+        if i % 2 == 0 and len(nz) >= 2:
+            a, b = rng.choice(nz, 2, replace=False)
+            odd[i, b] = odd[i, a]
+        else:
+            odd[i, rng.choice(81, 2, replace=False)] = rng.integers(10, 256, 2)
+    boards = np.concatenate([p30, sparse, odd, np.zeros((1, 81), np.uint8)])
+    lo = rng.integers(1, 10, len(boards))
+    hi = np.minimum(10, lo + rng.integers(1, 10, len(boards)))
+    masks = np.array([O.range_mask(int(a), int(b)) for a, b in zip(lo, hi)], dtype=np.uint16)
+    masks[: len(p30)] = O.range_mask(1, 10)
+    budget = 300_000
+    lane_engine.set_option(L.SDK_OPT_NODE_BUDGET, budget)
+    out, st, work = lane_engine.solve_batch(boards, masks, want_work=True)
+    ref_out, ref_st, ref_val = O.naive_solve_batch(boards, masks, budget=budget, threads=16)
+    assert (st == ref_st).all()
+    assert (out == ref_out).all()
+    assert (work == ref_val).all()
+    assert (st[: len(p30)] == 1).mean() > 0.9 and (st == -2).any() and (st == 0).any()
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 257, 5000])
+def test_ragged_batches(lane_engine, n):
+    p, s = synth.make_30clue(n, seed=100 + n)
+    out, st, _ = lane_engine.solve_batch(p)
+    assert (st == 1).all() and (out == s).all()
+
+
+def test_lane_rejects_mrv(lane_engine):
+    lane_engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+    try:
+        with pytest.raises(Exception):
+            lane_engine.solve_batch(np.zeros((1, 81), np.uint8))
+    finally:
+        lane_engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)

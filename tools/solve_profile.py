@@ -18,8 +18,9 @@ ap.add_argument("--workload", default="solve17")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--stats", action="store_true")
 ap.add_argument("--waves-per-cu", type=int, default=0)
-ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave", "quad"])
+ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave", "quad", "lane"])
 ap.add_argument("--sweep", action="store_true", help="time waves-per-CU settings")
+ap.add_argument("--budget", type=int, default=0, help="SDK_OPT_NODE_BUDGET (LANE: reference validations)")
 ap.add_argument("--order", default="lex", choices=["mrv_unique", "lex"])
 ap.add_argument("--locked", type=int, default=1, help="QUAD: locked-candidates pass (SDK_OPT_LOCKED: 0 off, 1 root, 2 all nodes)")
 args = ap.parse_args()
@@ -33,8 +34,10 @@ with SudokuEngine(0) as eng:
     eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
     eng.set_option(L.SDK_OPT_LOCKED, args.locked)
     eng.set_option(L.SDK_OPT_SOLVER, {"halfwave": L.SDK_SOLVER_HALFWAVE, "wave": L.SDK_SOLVER_WAVE,
-                                      "quad": L.SDK_SOLVER_QUAD}[args.solver])
+                                      "quad": L.SDK_SOLVER_QUAD, "lane": L.SDK_SOLVER_LANE}[args.solver])
     wopt = L.SDK_OPT_WAVES_PER_CU if args.solver == "wave" else L.SDK_OPT_WAVES_PER_CU2
+    if args.budget:
+        eng.set_option(L.SDK_OPT_NODE_BUDGET, args.budget)
     if args.waves_per_cu:
         eng.set_option(wopt, args.waves_per_cu)
     d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)

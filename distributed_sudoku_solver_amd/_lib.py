@@ -37,6 +37,7 @@ SDK_OPT_SOLVE_CHUNK = 10
 SDK_OPT_TIMING = 11
 SDK_OPT_TIMER_EVENTS = 12
 SDK_OPT_LOCKED = 13
+SDK_OPT_XCD_HEADS = 14
 SDK_CHECK_REG1 = 0
 SDK_CHECK_REG2 = 1
 SDK_CHECK_GLDS2 = 2

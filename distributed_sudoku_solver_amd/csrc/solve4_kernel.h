@@ -55,14 +55,15 @@ namespace sdk {
 #define SDK_SOLVE4_LDS_LEVELS 0
 #endif
 #ifndef SDK_SOLVE4_WAVES_PER_EU
-#define SDK_SOLVE4_WAVES_PER_EU 7
+#define SDK_SOLVE4_WAVES_PER_EU 6
 #endif
 // DFS levels kept in LDS (per level: 2 slots x 64 lanes x 8 B = 1 KiB; deeper levels go
-// to the per-workgroup global stack).  Default 0: a 17-clue board branches 1.65 times
-// on average, so the stack is cold, and the 4.4 KiB block lets occupancy follow the
-// VGPR budget -- 7 waves per SIMD at 72 VGPRs measured best (4M 17-clue puzzles:
-// 2 levels / 6 waves 692M/s, 0 / 7 731M/s, 0 / 8 715M/s, the last spilling outside
-// the round).
+// to the per-workgroup global stack).  Default 0: a 17-clue board rarely branches, so the
+// stack is cold, and the 4.5 KiB block lets occupancy follow the VGPR budget.  Waves per
+// SIMD: 7 (72 VGPRs) measured best until the per-XCD dequeue heads; with them the round's
+// LDS addresses spill at 72 VGPRs (reloaded every round), and 6 waves at 80 VGPRs without
+// spills is faster (A/B, 4M puzzles: 17-clue 831 vs 796M/s, 30-clue 1547 vs 1484M/s,
+// minimal 511 vs 499M/s).
 constexpr int kLds4Levels = SDK_SOLVE4_LDS_LEVELS;
 
 // Profiling build only (tools/build_variant.sh prof -DSDK_SOLVE4_PROFILE=1,
@@ -381,6 +382,7 @@ struct Slot4 {
     uint32_t depth, order, count, lim;
     uint32_t rstart, active;
     uint32_t maxd;            // deepest DFS level reached (SDK_WORK_DEPTH)
+    uint32_t seg, drained;    // dequeue segment (heads) and how many segments were found drained
     uint64_t nodes;
 };
 
@@ -405,6 +407,8 @@ __device__ __forceinline__ uint32_t snap_s4(uint32_t y) {
 struct Args4 : Args2 {
     uint32_t iter;
     int locked;
+    uint32_t* heads;
+    uint32_t seg_size;        // boards per dequeue segment (heads)
 };
 
 // Locked candidates (pointing and claiming) for the board in slot HI, run at its
@@ -543,11 +547,31 @@ template <int HI>
 __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c) {
     ++b.bidx;
     if (b.bidx >= b.bend) {
-        uint32_t base = 0;
-        if (w.hl == 0) base = atomicAdd(a.next, a.chunk);
-        base = half_first4(w, base);
-        b.bidx = base;
-        b.bend = (uint32_t)min((uint64_t)base + a.chunk, a.n);
+        if (a.heads) {
+            // XCD-local segment first, then the others in turn (see kHeads)
+            for (;;) {
+                const uint32_t lo = b.seg * a.seg_size, hi = min(lo + a.seg_size, (uint32_t)a.n);
+                uint32_t off = 0;
+                if (w.hl == 0) off = atomicAdd(a.heads + b.seg * kHeadStride, a.chunk);
+                off = half_first4(w, off);
+                if ((uint64_t)lo + off < hi) {
+                    b.bidx = lo + off;
+                    b.bend = min(b.bidx + a.chunk, hi);
+                    break;
+                }
+                if (++b.drained >= (uint32_t)kHeads) {
+                    b.bidx = b.bend = (uint32_t)a.n;
+                    break;
+                }
+                b.seg = (b.seg + 1) % kHeads;
+            }
+        } else {
+            uint32_t base = 0;
+            if (w.hl == 0) base = atomicAdd(a.next, a.chunk);
+            base = half_first4(w, base);
+            b.bidx = base;
+            b.bend = (uint32_t)min((uint64_t)base + a.chunk, a.n);
+        }
     }
     b.active = (uint64_t)b.bidx < a.n ? 1u : 0u;
     b.order = a.order == ORDER_LEX ? ORDER_LEX : ORDER_MRV;
@@ -607,8 +631,10 @@ __device__ __forceinline__ void lex_pick4(const Lane4& w, uint32_t x0, uint32_t 
     uint32_t cl[2], ml[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        const uint32_t a0 = (uint32_t)(o0 >> (32 * h)), a1 = (uint32_t)(o1 >> (32 * h)),
-                       a2 = (uint32_t)(o2 >> (32 * h));
+        uint32_t a0 = (uint32_t)(o0 >> (32 * h)), a1 = (uint32_t)(o1 >> (32 * h)), a2 = (uint32_t)(o2 >> (32 * h));
+        // keep the halves 32-bit scalars: left alone, clang tests "high half != 0" as a 64-bit
+        // VALU compare against a constant it then holds in a VGPR pair for the whole kernel
+        asm("" : "+s"(a0), "+s"(a1), "+s"(a2));
         if (a0 != 0u) {
             const uint32_t l = __builtin_ctz(a0);
             cl[h] = l;
@@ -766,6 +792,8 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
     Slot4 b;
     b.bidx = 0xFFFFFFFFu;   // ++ -> 0 >= bend = 0: first dequeue
     b.bend = 0;
+    b.seg = blockIdx.x % kHeads;
+    b.drained = 0;
     b.depth = 0;
     b.count = 0;
     next_board4<HI>(w, w, a, b, c);
@@ -802,6 +830,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     a.budget = args.budget;
     a.iter = 0;
     a.locked = args.locked;
+    a.heads = args.heads;
+    a.seg_size = (uint32_t)((args.n + kHeads - 1) / kHeads);
 
     Cells4 c;
     c.x0 = c.x1 = c.x2 = 0u;

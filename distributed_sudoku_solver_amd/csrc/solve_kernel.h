@@ -77,7 +77,14 @@ struct SolveArgs {
     uint64_t in_first;         // board i of the launch reads in[(in_first + i*in_step)*81];
     uint64_t in_step;          // outputs stay dense (out[i*81], status[i]); 0/1 = contiguous
     int locked;                // QUAD solver: locked-candidates pass at fixpoints (SDK_OPT_LOCKED)
+    uint32_t* heads;           // QUAD solver: kHeads dequeue heads, one per XCD segment (nullable)
 };
+
+// per-XCD dequeue: the batch is cut into kHeads contiguous segments, workgroup g starts
+// on segment g % kHeads (the XCD round-robin dispatch puts it there) and moves to the
+// next segment when its own is drained; heads kHeadStride words apart (own cache lines)
+constexpr int kHeads = 8;
+constexpr int kHeadStride = 64;
 
 __device__ __forceinline__ uint32_t cell_init(uint32_t v) {
     return v == 0 ? kCands : (v <= 9 ? ((1u << (v - 1)) | kClue) : kInert);

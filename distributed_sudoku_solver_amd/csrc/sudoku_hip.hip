@@ -75,10 +75,11 @@ struct sdk_ctx {
     int work_rounds = 0;
     int solver = SDK_SOLVER_QUAD;
     int locked = 1;                // QUAD: locked candidates at fixpoints (fewer search nodes, same answers)
-    int waves_per_cu2 = 32;       // solve2/solve4 grid per CU (24 resident: 80 VGPRs, <= 6.8 KB LDS; the rest
-                                  // start as the first retire, and the smaller dequeue chunk trims the tail)
+    int waves_per_cu2 = 24;       // solve2/solve4 grid per CU = the resident waves (80 VGPRs: 6 per SIMD; a larger
+                                  // grid only adds waves that start once the queue is drained: 1 % slower, r02)
     // workspaces
-    DevBuf stack, counter, in, mask, out, status, work, verdict;
+    DevBuf stack, counter, heads, in, mask, out, status, work, verdict;
+    int xcd_heads = 1;             // QUAD: per-XCD dequeue heads (SDK_OPT_XCD_HEADS)
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
     // the device-resident frontier of the last sdk_frontier_build (in fr_a)
     uint64_t fr_size = 0;
@@ -231,6 +232,13 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.in_first = in_first;
     a.in_step = in_step;
     a.locked = c->locked;
+    a.heads = nullptr;
+    if (four && c->xcd_heads && !count_mode) {
+        rc = ensure(c->heads, sdk::kHeads * sdk::kHeadStride * sizeof(uint32_t));
+        if (rc) return rc;
+        HIPCALL(hipMemsetAsync(c->heads.p, 0, sdk::kHeads * sdk::kHeadStride * sizeof(uint32_t), c->stream));
+        a.heads = static_cast<uint32_t*>(c->heads.p);
+    }
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
     if (rc) return rc;
@@ -506,6 +514,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 0 || value > 2) return fail(SDK_EINVAL, "locked must be 0, 1 or 2");
             c->locked = (int)value;
             return SDK_OK;
+        case SDK_OPT_XCD_HEADS:
+            if (value != 0 && value != 1) return fail(SDK_EINVAL, "xcd heads must be 0 or 1");
+            c->xcd_heads = (int)value;
+            return SDK_OK;
         case SDK_OPT_CHECK_VARIANT:
             if (value < SDK_CHECK_REG1 || value > SDK_CHECK_GLDS4) return fail(SDK_EINVAL, "bad check variant %lld", (long long)value);
             c->check_variant = (int)value;
@@ -531,6 +543,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_SOLVE_CHUNK: *value = c->solve_chunk; return SDK_OK;
         case SDK_OPT_TIMING: *value = c->timing ? 1 : 0; return SDK_OK;
         case SDK_OPT_LOCKED: *value = c->locked; return SDK_OK;
+        case SDK_OPT_XCD_HEADS: *value = c->xcd_heads; return SDK_OK;
         case SDK_OPT_TIMER_EVENTS: *value = (int64_t)c->events.size(); return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }

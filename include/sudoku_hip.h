@@ -69,7 +69,7 @@ extern "C" {
 #define SDK_OPT_WORK_COUNTER 5  /* what solve `work` counts: SDK_WORK_* (default nodes) */
 #define SDK_OPT_DEVICE_CUS   6  /* read-only: compute units of the context's GPU        */
 #define SDK_OPT_SOLVER       7  /* solve kernel: SDK_SOLVER_* (default QUAD)             */
-#define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE / QUAD solver per CU, 1..32 (default 32) */
+#define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE / QUAD solver per CU, 1..32 (default 24) */
 #define SDK_OPT_CHECK_VARIANT 9 /* checker tile pipeline: SDK_CHECK_* (default REG1) */
 #define SDK_OPT_SOLVE_CHUNK  10  /* boards per solver dequeue, 0 = automatic (default)  */
 #define SDK_OPT_TIMING       11  /* 1 = bracket every kernel with HIP events for        */
@@ -79,6 +79,8 @@ extern "C" {
                                  /* claiming) at propagation fixpoints before branching: */
                                  /* 0 never, 1 at the root node only (default), 2 at     */
                                  /* every node; same answers, fewer search nodes         */
+#define SDK_OPT_XCD_HEADS    14  /* QUAD solver: 1 = one dequeue head per XCD segment of */
+                                 /* the batch (default), 0 = one shared head             */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

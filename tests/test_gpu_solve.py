@@ -486,3 +486,19 @@ def test_locked_candidates_same_answers_fewer_nodes(engine, order):
     assert (st1[done] == st0[done]).all() and (o1[done] == o0[done]).all()
     assert (w1[:n17] == 1).all(), np.bincount(w1[:n17].astype(np.int64))
     assert w1[n17:n17 + nmin].mean() < w0[n17:n17 + nmin].mean()
+
+
+@pytest.mark.parametrize("n", [1, 7, 9, 1000, 100_003])
+def test_xcd_heads_same_boards(engine, n):
+    """Per-XCD dequeue segments (SDK_OPT_XCD_HEADS, default on) and one shared head solve
+    every board of the batch the same way, whatever the batch size vs the 8 segments."""
+    p, s = synth.make_17clue(n, seed=4000 + n)
+    res = {}
+    try:
+        for xh in (1, 0):
+            engine.set_option(L.SDK_OPT_XCD_HEADS, xh)
+            res[xh] = engine.solve_batch(p, want_work=True)
+    finally:
+        engine.set_option(L.SDK_OPT_XCD_HEADS, 1)
+    assert (res[1][1] == 1).all() and (res[1][0] == s).all()
+    assert (res[0][0] == res[1][0]).all() and (res[0][2] == res[1][2]).all()

@@ -409,6 +409,12 @@ struct Args4 : Args2 {
     int locked;
     uint32_t* heads;
     uint32_t seg_size;        // boards per dequeue segment (heads)
+    // count mode (frontier counts): every completion of each board is counted (MRV order,
+    // same propagation), summed into *count; no boards are written
+    int count_mode;
+    uint32_t count_lim;       // per-board stop: the count limit, or the flush point 2^31
+    bool count_stop;          // count_lim is the caller's limit (stop there), not a flush point
+    unsigned long long* count;
 };
 
 // Locked candidates (pointing and claiming) for the board in slot HI, run at its
@@ -574,8 +580,8 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
         }
     }
     b.active = (uint64_t)b.bidx < a.n ? 1u : 0u;
-    b.order = a.order == ORDER_LEX ? ORDER_LEX : ORDER_MRV;
-    b.lim = b.order == ORDER_LEX ? 1u : 2u;
+    b.order = (a.order == ORDER_LEX && !a.count_mode) ? ORDER_LEX : ORDER_MRV;
+    b.lim = a.count_mode ? a.count_lim : (b.order == ORDER_LEX ? 1u : 2u);
     b.nodes = 0;
     b.maxd = 0;
     b.rstart = a.iter;
@@ -596,7 +602,9 @@ template <int HI>
 __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c,
                                               int st) {
     uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
-    if (st != 1 && w.act) {           // the reference restores the grid (DHT_Node.py:535)
+    if (a.count_mode && w.hl == 0 && st != -2 && b.count)
+        atomicAdd(a.count, (unsigned long long)b.count);
+    if (st != 1 && w.act && a.out) {  // the reference restores the grid (DHT_Node.py:535)
         const uint8_t* sin = w.s_in + HI * 81;
         dst[w.c0] = sin[w.c0];
         dst[w.c0 + 27] = sin[w.c0 + 27];
@@ -683,7 +691,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
     }
     if (r == P_SOLVED) {
         ++b.count;
-        if (b.count == 1 && w.act) {
+        if (b.count == 1 && w.act && a.out) {
             uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
             const uint8_t* sin = w.s_in + HI * 81;
             const uint32_t i0 = sin[w.c0], i1 = sin[w.c0 + 27], i2 = sin[w.c0 + 54];
@@ -691,12 +699,16 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
             dst[w.c0 + 27] = (uint8_t)(i1 == 0 ? (uint32_t)__ffs(s1) : i1);
             dst[w.c0 + 54] = (uint8_t)(i2 == 0 ? (uint32_t)__ffs(s2) : i2);
         }
-        if (b.count >= b.lim) {
-            if (b.order == ORDER_MRV) {      // >= 2 completions: lex re-search
+        if (b.count >= b.lim && a.count_mode && !a.count_stop) {
+            // 2^31 completions on one board: move all but one to the total and go on
+            if (w.hl == 0) atomicAdd(a.count, (unsigned long long)(b.count - 1u));
+            b.count = 1;
+        } else if (b.count >= b.lim) {
+            if (b.order == ORDER_MRV && !a.count_mode) {      // >= 2 completions: lex re-search
                 b.order = ORDER_LEX;
                 b.lim = 1;
                 start_board4<HI>(w, a, b, c, false);
-            } else {
+            } else {                                           // found, or the count limit
                 PROF4(3, finish_board4<HI>(w, wr, a, b, c, 1));
             }
             return;
@@ -831,6 +843,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     a.iter = 0;
     a.locked = args.locked;
     a.heads = args.heads;
+    a.count_mode = args.count_mode;
+    a.count_stop = args.count_mode && args.limit && args.limit < 0x80000000ull;
+    a.count_lim = a.count_stop ? (uint32_t)args.limit : 0x80000000u;
+    a.count = args.count;
     a.seg_size = (uint32_t)((args.n + kHeads - 1) / kHeads);
 
     Cells4 c;

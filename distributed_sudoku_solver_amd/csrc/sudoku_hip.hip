@@ -191,9 +191,13 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     }
     // two (solve2_kernel) or four (solve4_kernel) boards per wave for solves; count mode stays
     // one board per wave
-    const int per_wave = count_mode ? 1 : (c->solver == SDK_SOLVER_QUAD ? 4 : (c->solver == SDK_SOLVER_HALFWAVE ? 2 : 1));
+    // count mode: QUAD counts four boards per wave (solve4's count mode) unless per-board counts
+    // are asked for; the other solvers count with the one-board-per-wave kernel
+    const int per_wave = count_mode ? ((c->solver == SDK_SOLVER_QUAD && !d_counts) ? 4 : 1)
+                                    : (c->solver == SDK_SOLVER_QUAD ? 4 : (c->solver == SDK_SOLVER_HALFWAVE ? 2 : 1));
     const bool two = per_wave == 2, four = per_wave == 4;
-    if ((two || four) && (!d_out || !d_status)) return fail(SDK_EINVAL, "solve needs out and status buffers");
+    if ((two || four) && !d_status) return fail(SDK_EINVAL, "solve needs a status buffer");
+    if ((two || four) && !count_mode && !d_out) return fail(SDK_EINVAL, "solve needs an out buffer");
     const uint64_t slots = (uint64_t)c->cus * (per_wave > 1 ? c->waves_per_cu2 : c->waves_per_cu) * per_wave;
     // 16 boards per dequeue (fewer when a slot would get < 2 dequeues).  All dequeues hit ONE
     // counter and same-address atomics serialise at ~10 ns each: below ~16 boards the cheap
@@ -233,7 +237,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.in_step = in_step;
     a.locked = c->locked;
     a.heads = nullptr;
-    if (four && c->xcd_heads && !count_mode) {
+    if (four && c->xcd_heads) {
         rc = ensure(c->heads, sdk::kHeads * sdk::kHeadStride * sizeof(uint32_t));
         if (rc) return rc;
         HIPCALL(hipMemsetAsync(c->heads.p, 0, sdk::kHeads * sdk::kHeadStride * sizeof(uint32_t), c->stream));

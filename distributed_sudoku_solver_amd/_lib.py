@@ -88,6 +88,7 @@ SIGNATURES = {
                                                  ctypes.POINTER(ctypes.c_int8)]),
     "sdk_frontier_build": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "sdk_frontier_refine": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]),
     "sdk_frontier_count_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                               ctypes.c_uint64, _vp]),
     "sdk_frontier_first_dev": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp]),

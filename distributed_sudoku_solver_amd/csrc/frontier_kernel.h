@@ -282,6 +282,15 @@ __global__ __launch_bounds__(64) void emit_kernel(const uint8_t* __restrict__ pr
 // status[0..n) of frontier boards lo .. lo+n-1 (dense).  found <- lo + the first i
 // whose status is not 0 (solved, or budget hit: either ends a lex-ordered scan),
 // INT64_MAX if none; best[0..80] <- that board's output, best[81] <- its status.
+// out[k] = in[first + k * step] (81-byte boards), k < n: a rank's share of a frontier
+__global__ __launch_bounds__(256) void gather_boards_kernel(const uint8_t* __restrict__ in, uint64_t first,
+                                                            uint64_t step, uint64_t n, uint8_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n * 81; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t b = i / 81, k = i - b * 81;
+        out[i] = in[(first + b * step) * 81 + k];
+    }
+}
+
 __global__ __launch_bounds__(256) void first_hit_kernel(const int8_t* __restrict__ status,
                                                         const uint8_t* __restrict__ out, uint64_t n, uint64_t lo,
                                                         long long* found, uint8_t* best) {

@@ -265,29 +265,37 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
 //   SDK_FRONTIER_FIRST: lex branching, solved leaves kept in place, so the frontier is
 //                       in lex order of completions (see frontier_kernel.h).
 // Expansion stops once the frontier holds >= target boards (or nothing branches).
-int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, int mode, uint64_t target) {
+// Breadth-first expansion of the frontier in fr_a (m0 boards; level 0 applies the
+// first-cell mask in fr_mask when `use_mask`) until it reaches `target` boards.  Buffers
+// are sized once for the whole build, so the levels are enqueued without the host: a level
+// is expanded only while the frontier is below `target` (or at level 0), and a level with
+// more than `cap` children is rejected.
+constexpr uint64_t kFrontierCap = 1ull << 25;  // 32M boards (2.6 GB) per frontier buffer
+
+// boards a frontier buffer must hold for a build from m0 boards towards `target`
+uint64_t frontier_capacity(uint64_t m0, uint64_t target) {
+    const uint64_t m_exp = std::max<uint64_t>(m0, std::min(target, kFrontierCap));
+    return std::max<uint64_t>(1, std::min(kFrontierCap, 9 * m_exp));
+}
+
+// The caller has put the m0 boards in fr_a, sized for frontier_capacity(m0, target) boards
+// BEFORE seeding it (a later grow would drop them).
+int run_frontier_levels(sdk_ctx* c, uint64_t m0, bool use_mask, int mode, uint64_t target) {
     int rc;
-    c->fr_valid = false;
-    if (target == 0) target = (uint64_t)c->cus * (uint64_t)c->waves_per_cu * 8ull;
-    const uint64_t cap = 1ull << 25;  // 32M boards (2.6 GB) per frontier buffer
     const bool first = mode == SDK_FRONTIER_FIRST;
-    // Buffers are sized once for the whole build, so the levels can be enqueued without
-    // the host: a level is expanded only while the frontier is below `target` (or at
-    // level 0), and a level with more than `cap` children is rejected.
-    const uint64_t m_exp = std::max<uint64_t>(1, std::min(target, cap));
-    const uint64_t c_out = std::max<uint64_t>(1, std::min(cap, 9 * m_exp));
+    const uint64_t m_exp = std::max<uint64_t>(m0, std::min(target, kFrontierCap));
+    const uint64_t c_out = frontier_capacity(m0, target);
     const uint64_t tiles = (m_exp + sdk::kScanTile - 1) / sdk::kScanTile;
-    if ((rc = ensure(c->fr_a, c_out * 81)) || (rc = ensure(c->fr_b, c_out * 81)) || (rc = ensure(c->fr_mask, 16)) ||
+    if (c->fr_a.bytes < c_out * 81) return fail(SDK_EINVAL, "frontier buffer not sized before seeding");
+    if ((rc = ensure(c->fr_b, c_out * 81)) || (rc = ensure(c->fr_mask, 16)) ||
         (rc = ensure(c->prop, m_exp * 81)) || (rc = ensure(c->bcell, m_exp)) || (rc = ensure(c->bmask, m_exp * 2)) ||
         (rc = ensure(c->nchild, m_exp * 4)) || (rc = ensure(c->offs, m_exp * 8)) || (rc = ensure(c->tsum, tiles * 8)) ||
         (rc = ensure(c->fr_ctl, sizeof(sdk::FrontierCtl))))
         return rc;
     sdk::FrontierCtl* ctl = static_cast<sdk::FrontierCtl*>(c->fr_ctl.p);
     sdk::FrontierCtl h{};
-    h.m = 1;
+    h.m = m0;
     HIPCALL(hipMemcpyAsync(ctl, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
-    HIPCALL(hipMemcpyAsync(c->fr_a.p, h_board, 81, hipMemcpyHostToDevice, c->stream));
-    if (h_mask) HIPCALL(hipMemcpyAsync(c->fr_mask.p, h_mask, 2, hipMemcpyHostToDevice, c->stream));
     void* buf[2] = {c->fr_a.p, c->fr_b.p};
     const unsigned eg = (unsigned)std::max<uint64_t>(
         1, std::min<uint64_t>((m_exp + sdk::kChunk - 1) / sdk::kChunk, (uint64_t)c->cus * c->waves_per_cu));
@@ -298,7 +306,7 @@ int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, i
     constexpr int kLevelsPerSync = 4;
     for (int level = 0; level < 81; ++level) {
         const int in = level & 1;
-        sdk::frontier_begin_kernel<<<1, 1, 0, c->stream>>>(ctl, target, level == 0 && h_mask ? 1 : 0);
+        sdk::frontier_begin_kernel<<<1, 1, 0, c->stream>>>(ctl, target, level == 0 && use_mask ? 1 : 0);
         sdk::ExpandArgs ea;
         ea.in = static_cast<const uint8_t*>(buf[in]);
         ea.ctl = ctl;
@@ -307,7 +315,7 @@ int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, i
         ea.bmask = static_cast<uint16_t*>(c->bmask.p);
         ea.nchild = static_cast<uint32_t*>(c->nchild.p);
         ea.order = first ? sdk::ORDER_LEX : sdk::ORDER_MRV;
-        ea.mask = (level == 0 && h_mask) ? static_cast<const uint16_t*>(c->fr_mask.p) : nullptr;
+        ea.mask = (level == 0 && use_mask) ? static_cast<const uint16_t*>(c->fr_mask.p) : nullptr;
         ea.keep_leaves = first ? 1 : 0;
         sdk::expand_kernel<<<eg, 64, 0, c->stream>>>(ea);
         sdk::scan_tiles_kernel<<<sg, 1024, 0, c->stream>>>(static_cast<uint32_t*>(c->nchild.p),
@@ -334,6 +342,47 @@ int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, i
     c->fr_levels = h.level;
     c->fr_valid = true;
     return SDK_OK;
+}
+
+int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, int mode, uint64_t target) {
+    c->fr_valid = false;
+    if (target == 0) target = (uint64_t)c->cus * (uint64_t)c->waves_per_cu * 8ull;
+    int rc;
+    if ((rc = ensure(c->fr_a, frontier_capacity(1, target) * 81)) || (rc = ensure(c->fr_mask, 16))) return rc;
+    HIPCALL(hipMemcpyAsync(c->fr_a.p, h_board, 81, hipMemcpyHostToDevice, c->stream));
+    if (h_mask) HIPCALL(hipMemcpyAsync(c->fr_mask.p, h_mask, 2, hipMemcpyHostToDevice, c->stream));
+    return run_frontier_levels(c, 1, h_mask != nullptr, mode, target);
+}
+
+// Keep frontier boards first, first+step, ... of the current (count-mode) frontier and
+// expand them further, on this device alone, until they number `target`: the second,
+// rank-local stage of a frontier split, so a rank's share of a replicated frontier can be
+// small and cheap to build.  The leaves reported are those met during this refinement.
+int refine_frontier(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t target) {
+    if (!c->fr_valid) return fail(SDK_EINVAL, "no frontier: call sdk_frontier_build first");
+    if (step == 0) return fail(SDK_EINVAL, "step must be >= 1");
+    const uint64_t m = c->fr_size;
+    const uint64_t n = first < m ? (m - first + step - 1) / step : 0;
+    c->fr_valid = false;
+    target = std::max<uint64_t>(target, n);
+    int rc;
+    // fr_b takes the share and becomes fr_a: size it for the whole refinement now
+    if ((rc = ensure(c->fr_b, frontier_capacity(std::max<uint64_t>(n, 1), target) * 81))) return rc;
+    if (n) {
+        const unsigned g = (unsigned)std::min<uint64_t>((n + 3) / 4, (uint64_t)c->cus * 16);
+        sdk::gather_boards_kernel<<<g, 256, 0, c->stream>>>(static_cast<const uint8_t*>(c->fr_a.p), first, step, n,
+                                                           static_cast<uint8_t*>(c->fr_b.p));
+        HIPCALL(hipGetLastError());
+    }
+    std::swap(c->fr_a, c->fr_b);
+    if (n == 0) {
+        c->fr_size = 0;
+        c->fr_leaves = 0;
+        c->fr_levels = 0;
+        c->fr_valid = true;
+        return SDK_OK;
+    }
+    return run_frontier_levels(c, n, false, SDK_FRONTIER_COUNT, target);
 }
 
 // Count the completions below frontier boards first, first+step, ... < end into
@@ -388,6 +437,7 @@ int count_slice(sdk_ctx* c, const uint8_t* h_board, uint64_t limit, int rank, in
     if (rc) return rc;
     const uint64_t m = c->fr_size;
     const uint64_t lo = (rank * m) / world, hi = ((rank + 1) * m) / world;
+    if ((rc = ensure(c->counter, 256))) return rc;   // before taking an address inside it
     unsigned long long* d_res = static_cast<unsigned long long*>(c->counter.p) + 6;
     if ((rc = frontier_count(c, lo, 1, hi, limit, d_res))) return rc;
     unsigned long long res[2] = {0, 0};
@@ -719,6 +769,18 @@ int sdk_frontier_build(sdk_ctx* c, const uint8_t* board, const uint16_t* first_c
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
     int rc = build_frontier(c, board, first_cell_mask, mode, target);
+    if (rc) return rc;
+    if (size) *size = c->fr_size;
+    if (leaves) *leaves = c->fr_leaves;
+    return SDK_OK;
+}
+
+int sdk_frontier_refine(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t target, uint64_t* size,
+                        uint64_t* leaves) {
+    if (!c) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    int rc = refine_frontier(c, first, step, target);
     if (rc) return rc;
     if (size) *size = c->fr_size;
     if (leaves) *leaves = c->fr_leaves;

@@ -254,6 +254,15 @@ class SudokuEngine:
                                             ctypes.byref(size), ctypes.byref(leaves)), "sdk_frontier_build")
         return size.value, leaves.value
 
+    def frontier_refine(self, first, step, target):
+        """Keep frontier boards first, first+step, ... and expand them on this GPU until they
+        number `target` (the rank-local second stage of a split): (size, leaves met)."""
+        size = ctypes.c_uint64()
+        leaves = ctypes.c_uint64()
+        L.check(self.lib.sdk_frontier_refine(self.ctx, int(first), int(step), int(target), ctypes.byref(size),
+                                             ctypes.byref(leaves)), "sdk_frontier_refine")
+        return size.value, leaves.value
+
     def frontier_count(self, first, step, end, limit, d_result):
         """Completions below frontier boards first, first+step, ... < end -> d_result {count, budget hits}."""
         L.check(self.lib.sdk_frontier_count_dev(self.ctx, int(first), int(step), int(end), int(limit), d_result.ptr),

@@ -324,29 +324,59 @@ def default_target(engine, world):
     return engine.get_option(L.SDK_OPT_DEVICE_CUS) * engine.get_option(L.SDK_OPT_WAVES_PER_CU) * 8 * world
 
 
-def sharded_count(engine, board, rank, world, limit=0, comm=None, target=None):
+def sharded_count(engine, board, rank, world, limit=0, comm=None, target=None, refine=True):
     """Count the completions of `board` with `world` ranks (one GPU each).
+
+    world == 1 (or refine=False): one frontier of `target` boards, rank k counting boards
+    k, k + world, ...  world > 1: a two-stage split -- every rank expands the same SMALL
+    frontier (1024 boards per rank), takes its interleaved share and grows that on its own
+    GPU to one GPU's frontier (engine.frontier_refine), so the replicated part does not grow
+    with the world size.  Completions met while expanding are counted once: those of the
+    replicated stage by rank 0, those of a refinement by its rank.
 
     Returns (total, status, frontier_size); status 1 = >= 1 completion, 0 = none,
     -2 = some subtree hit the node budget (total is then a lower bound)."""
     if world > 1 and comm is None:
         raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
-    size, leaves = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT,
-                                         target=default_target(engine, world) if target is None else target)
+    two_stage = world > 1 and refine and hasattr(engine, "frontier_refine")
+    if two_stage:
+        size, leaves0 = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT, target=1024 * world)
+        mine, leaves1 = engine.frontier_refine(rank, world, default_target(engine, 1) if target is None else target)
+        first, step, end = 0, 1, mine
+        own_leaves = leaves1 + (leaves0 if rank == 0 else 0)
+    else:
+        size, leaves = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT,
+                                             target=default_target(engine, world) if target is None else target)
+        first, step, end = rank, world, size
+        own_leaves = None
     res = engine.result_buffer(2, np.uint64)
     try:
-        engine.frontier_count(rank, world, size, limit, res)       # boards rank, rank+world, ...
+        engine.frontier_count(first, step, end, limit, res)
+        if two_stage:   # this rank's leaves ride in the same all-reduce
+            _add_to_result(engine, res, own_leaves)
         if comm is not None:
             comm.allreduce(res, 2, np.uint64, "sum")
         count, hits = (int(x) for x in engine.read(res, 2, np.uint64))
     finally:
         if hasattr(res, "free"):
             res.free()
-    total = count + leaves                                         # leaves: same on every rank
+    total = count + (0 if two_stage else leaves)                   # single stage: leaves are on every rank
     if limit and total > limit:
         total = limit
     st = -2 if hits else (1 if total > 0 else 0)
     return total, st, size
+
+
+def _add_to_result(engine, res, k):
+    """res[0] += k (the 2 x u64 result buffer is a device buffer, or a host array for doubles)."""
+    if not k:
+        return
+    vals = np.asarray(engine.read(res, 2, np.uint64), dtype=np.uint64).copy()
+    vals[0] += np.uint64(k)
+    if hasattr(res, "upload"):
+        res.upload(vals)
+    else:
+        res[:2] = vals
 
 
 def sharded_solve(engine, board, rank, world, comm=None, mask=None, waves=8, target=None):

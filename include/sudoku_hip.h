@@ -175,6 +175,14 @@ int sdk_frontier_build(sdk_ctx *ctx, const uint8_t *board, const uint16_t *first
 /* Count mode: completions below frontier boards first, first+step, ... < end,
  * written to d_result (device, 2 x uint64): {count, boards that hit the node
  * budget}.  The per-board search stops the batch once count >= limit (0 = none). */
+/* Second, rank-local stage of a frontier split (count mode): keep boards first,
+ * first+step, ... of the frontier built last and expand them further on this device
+ * until they number `target` (or nothing branches); *size / *leaves = the refined
+ * frontier and the completions met while refining (this rank's alone).  A rank can so
+ * take its share of a small replicated frontier and grow it locally, instead of every
+ * rank expanding a world-sized frontier. */
+int sdk_frontier_refine(sdk_ctx *ctx, uint64_t first, uint64_t step, uint64_t target, uint64_t *size,
+                        uint64_t *leaves);
 int sdk_frontier_count_dev(sdk_ctx *ctx, uint64_t first, uint64_t step, uint64_t end, uint64_t limit,
                            void *d_result);
 

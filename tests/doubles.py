@@ -28,8 +28,17 @@ class OracleEngine:
     def frontier_build(self, board, mask=None, mode=L.SDK_FRONTIER_COUNT, target=0):
         """Naive-DFS order expansion (lowest empty cell, digits ascending, utils.py:14-56)
         without propagation, level by level until >= target boards."""
-        fr = [np.asarray(board, dtype=np.uint8).copy()]
-        allowed0 = mask
+        self.frontier = self._expand([np.asarray(board, dtype=np.uint8).copy()], target, mask)
+        return len(self.frontier), 0
+
+    def frontier_refine(self, first, step, target):
+        """This rank's boards first, first+step, ... of the frontier, expanded on until >= target."""
+        self.calls.append(("refine", first, step, len(self.frontier)))
+        self.frontier = self._expand(list(self.frontier[first::step]), target, None)
+        return len(self.frontier), 0
+
+    @staticmethod
+    def _expand(fr, target, allowed0):
         while fr and len(fr) < max(target, 1):
             nxt, grew = [], False
             for b in fr:
@@ -54,8 +63,7 @@ class OracleEngine:
             fr = nxt
             if not grew:
                 break
-        self.frontier = fr
-        return len(fr), 0
+        return fr
 
     def result_buffer(self, count, dtype):
         return np.zeros(count, dtype=dtype)

@@ -46,7 +46,14 @@ def _worker(rank, world, port, q):
         s1 = synth.SEEDS17["S1"]
         q.put(("calls", rank, list(eng.calls)))
         eng.calls = []
+        # two-stage split (default): shares of a small replicated frontier, refined per rank
         total, st, size = sharded_count(eng, synth.parse(s1[:-9] + "000800000"), rank, world, comm=comm)
+        ref = [c for c in eng.calls if c[0] == "refine"]
+        q.put(("count_refine", rank, ref[0][1:] if ref else None, total == 7309 and st == 1))
+        # single stage: interleaved boards of one replicated frontier
+        eng.calls = []
+        total, st, size = sharded_count(eng, synth.parse(s1[:-9] + "000800000"), rank, world, comm=comm,
+                                        refine=False)
         counted = [c[1] for c in eng.calls if c[0] == "count"][0]
         if rank == 0:
             q.put(("count", total == 7309 and st == 1 and size >= 32))
@@ -98,8 +105,8 @@ def test_world2_gloo_gather():
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    got = [q.get(timeout=5) for _ in range(3 + 6 * world)]
-    res = {g[0]: g[1:] for g in got if g[0] not in ("calls", "count_split", "first", "first_range", "unsolvable",
+    got = [q.get(timeout=5) for _ in range(3 + 7 * world)]
+    res = {g[0]: g[1:] for g in got if g[0] not in ("calls", "count_split", "count_refine", "first", "first_range", "unsolvable",
                                                     "rebal")}
     rebal = {g[1]: g[2:] for g in got if g[0] == "rebal"}
     assert rebal[0][0] and rebal[1][0]                                      # same total on both ranks
@@ -109,6 +116,9 @@ def test_world2_gloo_gather():
     assert res["solve"] == (True,) and res["check"] == (True,) and res["count"] == (True,)
     for key in ("first", "first_range", "unsolvable"):
         assert sorted(g[1:] for g in got if g[0] == key) == [(r, True) for r in range(world)], key
+    refs = {g[1]: g[2:] for g in got if g[0] == "count_refine"}
+    assert refs[0][1] and refs[1][1]                                  # exact total on both ranks
+    assert refs[0][0][:2] == (0, 2) and refs[1][0][:2] == (1, 2)      # interleaved shares of stage 1
     split = {g[1]: g[2:] for g in got if g[0] == "count_split"}
     size = split[0][1]
     assert sorted(split[0][0] + split[1][0]) == list(range(size))     # interleaved, disjoint, complete

@@ -78,3 +78,30 @@ def test_lane_rejects_mrv(lane_engine):
             lane_engine.solve_batch(np.zeros((1, 81), np.uint8))
     finally:
         lane_engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
+
+
+def test_mixin_counts_reference_validations(lane_engine, solve_cases):
+    """A node whose engine runs the LANE solver advances `validations` exactly as the
+    reference's DHTNode does (DHT_Node.py:513,527-531; the /stats "validation" key)."""
+    import queue
+    from distributed_sudoku_solver_amd.solver import HipSolveMixin
+
+    class Node(HipSolveMixin):
+        def __init__(self, engine):
+            self.task = {"uuid": 0}
+            self.neighbor = None
+            self.neighborfree = False
+            self.validations = 0
+            self.task_queue = queue.Queue()
+            self.neighbor_tasks = queue.Queue()
+            self.sudoku_engine = engine
+
+        def non_blocking_receive(self):
+            return None, None
+
+    for c in [x for x in solve_cases if x["ok"]][:20]:
+        node = Node(lane_engine)
+        grid = [list(c["puzzle"][9 * r: 9 * r + 9]) for r in range(9)]
+        assert node.solve_sudoku(grid, 0, range(*c["range"])) is True
+        assert [v for row in grid for v in row] == c["board"], c["name"]
+        assert node.validations == c["validations"], c["name"]

@@ -13,9 +13,11 @@ Node protocol side effects of the reference's recursive solver are applied once,
 before the (micro-second) device call instead of once per recursion level:
 cancellation (`task == []`, DHT_Node.py:481), one non-blocking UDP poll
 (DHT_Node.py:485-488), and the hand-off of half the digit range to a free
-neighbour (DHT_Node.py:491-510).  `validations` is advanced by the engine's own
-search-node counter (the naive-DFS count is not defined for a propagating
-search).
+neighbour (DHT_Node.py:491-510).  `validations` is advanced by the engine's work counter:
+search nodes for the propagating solvers (the naive-DFS count is not defined for a
+propagating search), or exactly the reference's validations when the
+engine runs the one-board-per-lane reference DFS (SDK_OPT_SOLVER = SDK_SOLVER_LANE;
+slow on hard boards, exact /stats accounting).
 """
 import threading
 

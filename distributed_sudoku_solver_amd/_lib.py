@@ -127,7 +127,12 @@ def load():
             f"{LIB_PATH} not found: build it with `make -C distributed_sudoku_solver_amd/csrc` "
             "or `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(LIB_PATH)
+    # a library named by SDK_LIB_PATH (dev A/B builds of older commits) may predate newer
+    # entry points; the in-tree library must export every one
+    override = "SDK_LIB_PATH" in os.environ
     for name, (res, args) in SIGNATURES.items():
+        if override and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -55,15 +55,13 @@ namespace sdk {
 #define SDK_SOLVE4_LDS_LEVELS 0
 #endif
 #ifndef SDK_SOLVE4_WAVES_PER_EU
-#define SDK_SOLVE4_WAVES_PER_EU 6
+#define SDK_SOLVE4_WAVES_PER_EU 7
 #endif
 // DFS levels kept in LDS (per level: 2 slots x 64 lanes x 8 B = 1 KiB; deeper levels go
 // to the per-workgroup global stack).  Default 0: a 17-clue board rarely branches, so the
-// stack is cold, and the 4.5 KiB block lets occupancy follow the VGPR budget.  Waves per
-// SIMD: 7 (72 VGPRs) measured best until the per-XCD dequeue heads; with them the round's
-// LDS addresses spill at 72 VGPRs (reloaded every round), and 6 waves at 80 VGPRs without
-// spills is faster (A/B, 4M puzzles: 17-clue 831 vs 796M/s, 30-clue 1547 vs 1484M/s,
-// minimal 511 vs 499M/s).
+// stack is cold, and the 4.5 KiB block lets occupancy follow the VGPR budget: 7 waves per
+// SIMD at 72 VGPRs (A/B, 10M 17-clue puzzles: 890 vs 883M/s at 6 waves / 80 VGPRs; at 72 the
+// dequeue code must stay straight-line, or the round's LDS addresses spill, see next_board4).
 constexpr int kLds4Levels = SDK_SOLVE4_LDS_LEVELS;
 
 // Profiling build only (tools/build_variant.sh prof -DSDK_SOLVE4_PROFILE=1,
@@ -380,9 +378,8 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
 struct Slot4 {
     uint32_t bidx, bend;
     uint32_t depth, order, count, lim;
-    uint32_t rstart, active;
+    uint32_t rstart, active;  // active: bit 0 a board is loaded, bit 1 the home segment is drained (heads)
     uint32_t maxd;            // deepest DFS level reached (SDK_WORK_DEPTH)
-    uint32_t seg, drained;    // dequeue segment (heads) and how many segments were found drained
     uint64_t nodes;
 };
 
@@ -409,6 +406,8 @@ struct Args4 : Args2 {
     int locked;
     uint32_t* heads;
     uint32_t seg_size;        // boards per dequeue segment (heads)
+    uint32_t tail0;           // first board of the shared tail (heads)
+    uint32_t nseg;            // segments in use: min(kHeads, workgroups)
     // count mode (frontier counts): every completion of each board is counted (MRV order,
     // same propagation), summed into *count; no boards are written
     int count_mode;
@@ -554,23 +553,27 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
     ++b.bidx;
     if (b.bidx >= b.bend) {
         if (a.heads) {
-            // XCD-local segment first, then the others in turn (see kHeads)
-            for (;;) {
-                const uint32_t lo = b.seg * a.seg_size, hi = min(lo + a.seg_size, (uint32_t)a.n);
-                uint32_t off = 0;
-                if (w.hl == 0) off = atomicAdd(a.heads + b.seg * kHeadStride, a.chunk);
-                off = half_first4(w, off);
-                if ((uint64_t)lo + off < hi) {
-                    b.bidx = lo + off;
-                    b.bend = min(b.bidx + a.chunk, hi);
-                    break;
-                }
-                if (++b.drained >= (uint32_t)kHeads) {
-                    b.bidx = b.bend = (uint32_t)a.n;
-                    break;
-                }
-                b.seg = (b.seg + 1) % kHeads;
+            // XCD-local segment (see kHeads), then the shared tail: straight-line code, no
+            // segment-walking loop (its control flow alone made the allocator spill the
+            // round's LDS addresses at 72 VGPRs)
+            uint32_t base = 0, end = 0;
+            bool drained = (b.active & 2u) != 0u;
+            if (!drained) {
+                const uint32_t seg = blockIdx.x % a.nseg;   // the home segment (of this workgroup's XCD)
+                const uint32_t lo = seg * a.seg_size, hi = min(lo + a.seg_size, a.tail0);
+                if (w.hl == 0) base = atomicAdd(a.heads + seg * kHeadStride, a.chunk);
+                base = lo + half_first4(w, base);
+                end = hi;
+                drained = base >= hi;
             }
+            if (drained) {
+                if (w.hl == 0) base = atomicAdd(a.heads + kHeads * kHeadStride, a.chunk);
+                base = a.tail0 + half_first4(w, base);
+                end = (uint32_t)a.n;
+            }
+            b.bidx = min(base, (uint32_t)a.n);
+            b.bend = min(base + a.chunk, end);
+            b.active = drained ? 2u : 0u;
         } else {
             uint32_t base = 0;
             if (w.hl == 0) base = atomicAdd(a.next, a.chunk);
@@ -579,13 +582,13 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
             b.bend = (uint32_t)min((uint64_t)base + a.chunk, a.n);
         }
     }
-    b.active = (uint64_t)b.bidx < a.n ? 1u : 0u;
+    b.active = (b.active & 2u) | ((uint64_t)b.bidx < a.n ? 1u : 0u);
     b.order = (a.order == ORDER_LEX && !a.count_mode) ? ORDER_LEX : ORDER_MRV;
     b.lim = a.count_mode ? a.count_lim : (b.order == ORDER_LEX ? 1u : 2u);
     b.nodes = 0;
     b.maxd = 0;
     b.rstart = a.iter;
-    if (b.active) {
+    if (b.active & 1u) {
         start_board4<HI>(w, a, b, c, true);
     } else {
         c.x0 = setfld<HI>(c.x0, 0u);
@@ -795,7 +798,7 @@ __device__ __forceinline__ bool step4(const Lane4& wr, const Args4& a, Cells4& c
     Slot4* p = s_slot + w.half * 2 + HI;
     Slot4 b;
     PROF4(1 + HI, b = *p; step4_body<HI>(w, wr, a, b, c, bad, s_stk, g_stk); if (w.hl == 0) *p = b);
-    return b.active != 0u;
+    return (b.active & 1u) != 0u;
 }
 
 // first board of slot HI (all lanes)
@@ -804,13 +807,12 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
     Slot4 b;
     b.bidx = 0xFFFFFFFFu;   // ++ -> 0 >= bend = 0: first dequeue
     b.bend = 0;
-    b.seg = blockIdx.x % kHeads;
-    b.drained = 0;
+    b.active = 0;
     b.depth = 0;
     b.count = 0;
     next_board4<HI>(w, w, a, b, c);
     if (w.hl == 0) s_slot[w.half * 2 + HI] = b;
-    return b.active != 0u;
+    return (b.active & 1u) != 0u;
 }
 
 #ifdef SDK_DEFINE_SOLVE4_KERNEL   // defined in solve4_launch.hip only
@@ -847,7 +849,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     a.count_stop = args.count_mode && args.limit && args.limit < 0x80000000ull;
     a.count_lim = a.count_stop ? (uint32_t)args.limit : 0x80000000u;
     a.count = args.count;
-    a.seg_size = (uint32_t)((args.n + kHeads - 1) / kHeads);
+    {   // segments share the first n - n/32 boards (rounded to whole chunks); the rest is the tail
+        const uint64_t tail = ((args.n / 32 + args.chunk - 1) / args.chunk) * args.chunk;
+        a.tail0 = (uint32_t)(args.n - min<uint64_t>(tail, args.n));
+        // every segment needs a workgroup that drains it: fewer segments on a small grid
+        a.nseg = min<uint32_t>(kHeads, gridDim.x);
+        a.seg_size = (a.tail0 + a.nseg - 1) / a.nseg;
+    }
 
     Cells4 c;
     c.x0 = c.x1 = c.x2 = 0u;

@@ -80,9 +80,10 @@ struct SolveArgs {
     uint32_t* heads;           // QUAD solver: kHeads dequeue heads, one per XCD segment (nullable)
 };
 
-// per-XCD dequeue: the batch is cut into kHeads contiguous segments, workgroup g starts
-// on segment g % kHeads (the XCD round-robin dispatch puts it there) and moves to the
-// next segment when its own is drained; heads kHeadStride words apart (own cache lines)
+// per-XCD dequeue: the first n - n/32 boards are cut into kHeads contiguous segments with a
+// head each, workgroup g takes chunks of segment g % kHeads (the XCD the round-robin
+// dispatch put it on) and, once that is drained, of the shared tail (one more head);
+// heads kHeadStride words apart (own cache lines)
 constexpr int kHeads = 8;
 constexpr int kHeadStride = 64;
 

@@ -75,7 +75,7 @@ struct sdk_ctx {
     int work_rounds = 0;
     int solver = SDK_SOLVER_QUAD;
     int locked = 1;                // QUAD: locked candidates at fixpoints (fewer search nodes, same answers)
-    int waves_per_cu2 = 24;       // solve2/solve4 grid per CU = the resident waves (80 VGPRs: 6 per SIMD; a larger
+    int waves_per_cu2 = 28;       // solve2/solve4 grid per CU = solve4's resident waves (7 per SIMD; a larger
                                   // grid only adds waves that start once the queue is drained: 1 % slower, r02)
     // workspaces
     DevBuf stack, counter, heads, in, mask, out, status, work, verdict;
@@ -238,9 +238,9 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.locked = c->locked;
     a.heads = nullptr;
     if (four && c->xcd_heads) {
-        rc = ensure(c->heads, sdk::kHeads * sdk::kHeadStride * sizeof(uint32_t));
+        rc = ensure(c->heads, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t));
         if (rc) return rc;
-        HIPCALL(hipMemsetAsync(c->heads.p, 0, sdk::kHeads * sdk::kHeadStride * sizeof(uint32_t), c->stream));
+        HIPCALL(hipMemsetAsync(c->heads.p, 0, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t), c->stream));
         a.heads = static_cast<uint32_t*>(c->heads.p);
     }
     hipEvent_t stop;

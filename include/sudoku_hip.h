@@ -69,7 +69,7 @@ extern "C" {
 #define SDK_OPT_WORK_COUNTER 5  /* what solve `work` counts: SDK_WORK_* (default nodes) */
 #define SDK_OPT_DEVICE_CUS   6  /* read-only: compute units of the context's GPU        */
 #define SDK_OPT_SOLVER       7  /* solve kernel: SDK_SOLVER_* (default QUAD)             */
-#define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE / QUAD solver per CU, 1..32 (default 24) */
+#define SDK_OPT_WAVES_PER_CU2 8 /* grid of the HALFWAVE / QUAD solver per CU, 1..32 (default 28) */
 #define SDK_OPT_CHECK_VARIANT 9 /* checker tile pipeline: SDK_CHECK_* (default REG1) */
 #define SDK_OPT_SOLVE_CHUNK  10  /* boards per solver dequeue, 0 = automatic (default)  */
 #define SDK_OPT_TIMING       11  /* 1 = bracket every kernel with HIP events for        */

@@ -504,7 +504,7 @@ int sdk_destroy(sdk_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf* b : {&c->stack, &c->counter, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
+    for (DevBuf* b : {&c->stack, &c->counter, &c->heads, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
                       &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status,
                       &c->fr_mask, &c->tsum, &c->fr_ctl})
         if (b->p) (void)hipFree(b->p);

@@ -119,3 +119,10 @@ def test_int64_boards_vs_python_restatement(engine):
     assert (v & 1).any() and (v & 2).any()
     g = [[int(t) for t in boards[0][9 * r: 9 * r + 9]] for r in range(9)]
     assert Sudoku(g, engine=engine).check() == bool(v[0] & 1)
+
+
+def test_host_pointer_large_check(engine):
+    """A 3M-board host-pointer check batch: verdicts equal the expected ones."""
+    b, exp = synth.make_check_boards(3_000_000, seed=78)
+    v = engine.check_batch(b)
+    assert (v == exp).all()

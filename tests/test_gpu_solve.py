@@ -502,3 +502,12 @@ def test_xcd_heads_same_boards(engine, n):
         engine.set_option(L.SDK_OPT_XCD_HEADS, 1)
     assert (res[1][1] == 1).all() and (res[1][0] == s).all()
     assert (res[0][0] == res[1][0]).all() and (res[0][2] == res[1][2]).all()
+
+
+def test_host_pointer_large_batch(engine):
+    """A 2.5M-board host-pointer batch (sdk_solve_batch, masks and work): every board."""
+    n = 2_500_000
+    p, s = synth.make_17clue(n, seed=77)
+    masks = np.full(n, O.range_mask(1, 10), dtype=np.uint16)
+    out, st, work = engine.solve_batch(p, masks, want_work=True)
+    assert (st == 1).all() and (out == s).all() and (work >= 1).all()

@@ -488,6 +488,7 @@ def main():
         ndev = ctypes.c_int(0)
         L.check(L.load().sdk_device_count(ctypes.byref(ndev)), "sdk_device_count")
         eng = SudokuEngine(d.local_rank % max(1, ndev.value))
+        args.shared_gpus = d.world > ndev.value
     eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
     eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
     if args.waves_per_cu:
@@ -649,7 +650,11 @@ def main():
         bad_total += result["minimal_puzzles"]["parity"]["mismatched_boards"]
 
     # ------------------------------------------------------------ C5 leg
-    if args.count_leg:
+    if args.count_leg and getattr(args, "shared_gpus", False):
+        # RCCL refuses two ranks on one device ("invalid usage"): a rehearsal with more ranks than
+        # GPUs has no C5 leg (on a node every rank has its own GPU)
+        result["c5_count"] = {"skipped": "more ranks than GPUs: RCCL needs one device per rank"}
+    elif args.count_leg:
         result["c5_count"] = c5_leg(eng, d, synth)
         result["c5_count_rebalanced"] = c5_rebalanced_leg(eng, d, synth)
 

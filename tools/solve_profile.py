@@ -22,6 +22,7 @@ ap.add_argument("--solver", default="halfwave", choices=["halfwave", "wave", "qu
 ap.add_argument("--sweep", action="store_true", help="time waves-per-CU settings")
 ap.add_argument("--budget", type=int, default=0, help="SDK_OPT_NODE_BUDGET (LANE: reference validations)")
 ap.add_argument("--xcd-heads", type=int, default=-1, help="QUAD: SDK_OPT_XCD_HEADS (default: library default)")
+ap.add_argument("--chunk", type=int, default=0, help="SDK_OPT_SOLVE_CHUNK (0: automatic)")
 ap.add_argument("--order", default="lex", choices=["mrv_unique", "lex"])
 ap.add_argument("--locked", type=int, default=1, help="QUAD: locked-candidates pass (SDK_OPT_LOCKED: 0 off, 1 root, 2 all nodes)")
 args = ap.parse_args()
@@ -39,6 +40,8 @@ with SudokuEngine(0) as eng:
     wopt = L.SDK_OPT_WAVES_PER_CU if args.solver == "wave" else L.SDK_OPT_WAVES_PER_CU2
     if args.budget:
         eng.set_option(L.SDK_OPT_NODE_BUDGET, args.budget)
+    if args.chunk:
+        eng.set_option(L.SDK_OPT_SOLVE_CHUNK, args.chunk)
     if args.xcd_heads >= 0:
         eng.set_option(L.SDK_OPT_XCD_HEADS, args.xcd_heads)
     if args.waves_per_cu:
@@ -54,7 +57,7 @@ with SudokuEngine(0) as eng:
     ms, nl = eng.timer_read()
     out = np.empty((args.n, 81), np.uint8)
     d_out.download(out)
-    print(f"{args.solver} {args.order} lc={args.locked} xh={args.xcd_heads} {args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
+    print(f"{args.solver} {args.order} lc={args.locked} xh={args.xcd_heads} chunk={args.chunk} {args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
           f"ok={(out == s).all()}", flush=True)
     if args.sweep:
         for wpc in (8, 12, 16, 20, 24, 32):

@@ -54,6 +54,12 @@ namespace sdk {
 #ifndef SDK_SOLVE4_LDS_LEVELS
 #define SDK_SOLVE4_LDS_LEVELS 0
 #endif
+#ifndef SDK_SOLVE4_TAIL_DIV
+#define SDK_SOLVE4_TAIL_DIV 32        // the shared dequeue tail: n / this boards
+#endif
+#ifndef SDK_SOLVE4_TAIL_CHUNK_DIV
+#define SDK_SOLVE4_TAIL_CHUNK_DIV 1   // tail chunks: chunk / this boards
+#endif
 #ifndef SDK_SOLVE4_WAVES_PER_EU
 #define SDK_SOLVE4_WAVES_PER_EU 7
 #endif
@@ -408,6 +414,7 @@ struct Args4 : Args2 {
     uint32_t seg_size;        // boards per dequeue segment (heads)
     uint32_t tail0;           // first board of the shared tail (heads)
     uint32_t nseg;            // segments in use: min(kHeads, workgroups)
+    uint32_t tail_chunk;      // boards per dequeue from the shared tail
     // count mode (frontier counts): every completion of each board is counted (MRV order,
     // same propagation), summed into *count; no boards are written
     int count_mode;
@@ -567,12 +574,12 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
                 drained = base >= hi;
             }
             if (drained) {
-                if (w.hl == 0) base = atomicAdd(a.heads + kHeads * kHeadStride, a.chunk);
+                if (w.hl == 0) base = atomicAdd(a.heads + kHeads * kHeadStride, a.tail_chunk);
                 base = a.tail0 + half_first4(w, base);
                 end = (uint32_t)a.n;
             }
             b.bidx = min(base, (uint32_t)a.n);
-            b.bend = min(base + a.chunk, end);
+            b.bend = min(base + (drained ? a.tail_chunk : a.chunk), end);
             b.active = drained ? 2u : 0u;
         } else {
             uint32_t base = 0;
@@ -850,7 +857,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     a.count_lim = a.count_stop ? (uint32_t)args.limit : 0x80000000u;
     a.count = args.count;
     {   // segments share the first n - n/32 boards (rounded to whole chunks); the rest is the tail
-        const uint64_t tail = ((args.n / 32 + args.chunk - 1) / args.chunk) * args.chunk;
+        a.tail_chunk = max(1u, args.chunk / SDK_SOLVE4_TAIL_CHUNK_DIV);
+        const uint64_t tail = ((args.n / SDK_SOLVE4_TAIL_DIV + args.chunk - 1) / args.chunk) * args.chunk;
         a.tail0 = (uint32_t)(args.n - min<uint64_t>(tail, args.n));
         // every segment needs a workgroup that drains it: fewer segments on a small grid
         a.nseg = min<uint32_t>(kHeads, gridDim.x);

@@ -366,6 +366,17 @@ def lane_dfs_leg(eng, args, synth, L):
     finally:
         eng.set_option(L.SDK_OPT_NODE_BUDGET, 0)
         eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
+    # the same batch with the per-puzzle budget cut to 20k validations: the wave-parallel bulk
+    # rate without the serial tail of the few boards that need a million validations
+    eng.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_LANE)
+    eng.set_option(L.SDK_OPT_NODE_BUDGET, 20_000)
+    try:
+        t0 = time.perf_counter()
+        _, bst, bval = eng.solve_batch(p, want_work=True)
+        bwall = time.perf_counter() - t0
+    finally:
+        eng.set_option(L.SDK_OPT_NODE_BUDGET, 0)
+        eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
     m = min(n, 4096)
     cores = args.cpu_cores or cpu_share()
     t1 = time.perf_counter()
@@ -378,6 +389,9 @@ def lane_dfs_leg(eng, args, synth, L):
             "validations_per_puzzle": {"mean": float(val.mean()), "p99": float(np.percentile(val, 99)),
                                        "max": int(val.max())},
             "budget_hits": int((st == -2).sum()),
+            "bulk_20k_budget": {"solved_per_s": float((bst == 1).sum()) / bwall,
+                                "validations_per_s": float(bval.sum()) / bwall,
+                                "stopped_at_budget": int((bst == -2).sum()), "wall_ms": 1000.0 * bwall},
             "parity": {"mismatched_boards": int(((out != sol).any(axis=1) & ok).sum() + (~ok & (st != -2)).sum()),
                        "checked_boards": n,
                        "validations_vs_c_port": {"sample": m, "equal": int((val[:m] == ref_val).sum()),

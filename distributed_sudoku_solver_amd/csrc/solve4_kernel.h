@@ -54,6 +54,9 @@ namespace sdk {
 #ifndef SDK_SOLVE4_LDS_LEVELS
 #define SDK_SOLVE4_LDS_LEVELS 0
 #endif
+#ifndef SDK_SOLVE4_EXACT_UPD
+#define SDK_SOLVE4_EXACT_UPD 1        // exact waves also drop the two-hidden-singles test (upd4x)
+#endif
 #ifndef SDK_SOLVE4_TAIL_DIV
 #define SDK_SOLVE4_TAIL_DIV 32        // the shared dequeue tail: n / this boards
 #endif
@@ -262,6 +265,32 @@ __device__ __forceinline__ void upd4(uint32_t& X, uint32_t& S, uint32_t U, uint3
     X = xn;
 }
 
+// upd4 for waves whose boards are all exact (see unit4x): no "two hidden singles" test.
+// Such a cell keeps both digits as candidates, each the only place of its digit in some
+// unit; every completion then misses one of them, so the missing-digit test refutes each
+// branch on it -- only later, in states that are contradictory anyway.
+__device__ __forceinline__ void upd4x(uint32_t& X, uint32_t& S, uint32_t U, uint32_t H, uint32_t& bm, uint32_t& m,
+                                     uint32_t& chg) {
+    uint32_t xn, v1, h, t, v2;
+    asm("v_bitop3_b32 %[v1], %[x], %[u], %[u] bitop3:0x30\n\t"
+        "v_and_b32 %[h], %[v1], %[hh]\n\t"
+        "v_pk_sub_u16 %[t], 0, %[h]\n\t"
+        "v_pk_ashrrev_i16 %[t], 15, %[t] op_sel_hi:[0,1]\n\t"
+        "v_bitop3_b32 %[v2], %[h], %[v1], %[t] bitop3:0xf4\n\t"
+        "v_pk_add_u16 %[t], %[v2], -1\n\t"
+        "v_and_b32 %[t], %[v2], %[t]\n\t"
+        "v_or_b32 %[m], %[v2], %[s]\n\t"
+        "v_pk_add_u16 %[t], %[t], -1\n\t"
+        "v_pk_ashrrev_i16 %[t], 15, %[t] op_sel_hi:[0,1]\n\t"
+        "v_and_or_b32 %[s], %[v2], %[t], %[s]\n\t"
+        "v_bitop3_b32 %[xn], %[v2], %[t], %[t] bitop3:0x30\n\t"
+        "v_bitop3_b32 %[chg], %[chg], %[x], %[xn] bitop3:0xf6"
+        : [xn] "=&v"(xn), [v1] "=&v"(v1), [h] "=&v"(h), [t] "=&v"(t), [v2] "=&v"(v2), [m] "=&v"(m),
+          [s] "+v"(S), [bm] "+v"(bm), [chg] "+v"(chg)
+        : [x] "v"(X), [u] "v"(U), [hh] "v"(H));
+    X = xn;
+}
+
 // Unit summary of the lane's unit from its nine (X, S) cell words, one asm block.
 // "In two or more cells" is accumulated two cells at a time: a bit is set in at
 // least two of (acc, a, b) exactly when it is in their majority (bitop3 0xe8).
@@ -320,8 +349,42 @@ __device__ __forceinline__ uint32_t lds_addr4(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+// The unit summary when every board of the wave has only exact units (no duplicated
+// and no inert given; SDK_OPT_LOCKED != 0): no "taken twice" test and T = OR S.  A
+// digit taken twice in an exact unit leaves another digit of the unit with no cell, so
+// the missing-digit test still refutes every such state -- at the latest when its last
+// cell closes -- and no completion is accepted or lost.
+__device__ __forceinline__ void unit4x(const uint2 (&v)[9], uint32_t E, uint32_t& once, uint32_t& T, uint32_t& bm) {
+    uint32_t ox, os, t0, t1, t2, t3;
+    asm("v_or3_b32 %[ox], %[a0], %[a1], %[a2]\n\t"
+        "v_bitop3_b32 %[t0], %[a0], %[a1], %[a2] bitop3:0xe8\n\t"
+        "v_bitop3_b32 %[t1], %[ox], %[a3], %[a4] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a3], %[a4]\n\t"
+        "v_bitop3_b32 %[t2], %[ox], %[a5], %[a6] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a5], %[a6]\n\t"
+        "v_bitop3_b32 %[t3], %[ox], %[a7], %[a8] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a7], %[a8]\n\t"
+        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        "v_bitop3_b32 %[t0], %[ox], %[t0], %[t3] bitop3:0x10\n\t"
+        "v_and_b32 %[once], %[t0], %[e]\n\t"
+        "v_or3_b32 %[os], %[b0], %[b1], %[b2]\n\t"
+        "v_or3_b32 %[os], %[os], %[b3], %[b4]\n\t"
+        "v_or3_b32 %[os], %[os], %[b5], %[b6]\n\t"
+        "v_or3_b32 %[os], %[os], %[b7], %[b8]\n\t"
+        "v_bitop3_b32 %[bm], %[e], %[ox], %[os] bitop3:0x10"
+        : [ox] "=&v"(ox), [os] "=&v"(os), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [once] "=&v"(once), [bm] "=&v"(bm)
+        : [a0] "v"(v[0].x), [a1] "v"(v[1].x), [a2] "v"(v[2].x), [a3] "v"(v[3].x), [a4] "v"(v[4].x),
+          [a5] "v"(v[5].x), [a6] "v"(v[6].x), [a7] "v"(v[7].x), [a8] "v"(v[8].x),
+          [b0] "v"(v[0].y), [b1] "v"(v[1].y), [b2] "v"(v[2].y), [b3] "v"(v[3].y), [b4] "v"(v[4].y),
+          [b5] "v"(v[5].y), [b6] "v"(v[6].y), [b7] "v"(v[7].y), [b8] "v"(v[8].y),
+          [e] "v"(E));
+    T = os;
+}
+
 // One propagation round for all four boards, branch-free.  Out: per-lane packed
 // contradiction bits (bm, zmin) and change bits (chg).
+template <bool EXACT>
 __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, uint32_t& zmin, uint32_t& chg) {
     w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
     w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
@@ -331,7 +394,10 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
 #pragma unroll
     for (int k = 0; k < 9; ++k) v[k] = w.s_cell[w.ucell[k]];
     uint32_t once, T;
-    unit4(v, c.E, c.D, once, T, bm);
+    if (EXACT)
+        unit4x(v, c.E, once, T, bm);
+    else
+        unit4(v, c.E, c.D, once, T, bm);
     w.s_unit[w.c0] = make_uint2(T, once);
     wave_sync();
     uint32_t m0, m1, m2;
@@ -358,13 +424,13 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
         : "memory");
     asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(uc), "+v"(r0), "+v"(b0)::"memory");
     const uint32_t ucx = (uint32_t)uc, ucy = (uint32_t)(uc >> 32);
-    upd4(c.x0, c.s0, ucx | (uint32_t)r0 | (uint32_t)b0, ucy | (uint32_t)(r0 >> 32) | (uint32_t)(b0 >> 32), bm, m0,
+    ((EXACT && SDK_SOLVE4_EXACT_UPD) ? upd4x : upd4)(c.x0, c.s0, ucx | (uint32_t)r0 | (uint32_t)b0, ucy | (uint32_t)(r0 >> 32) | (uint32_t)(b0 >> 32), bm, m0,
          chg);
     asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(r1), "+v"(b1), "+v"(c.x0), "+v"(c.s0)::"memory");
-    upd4(c.x1, c.s1, ucx | (uint32_t)r1 | (uint32_t)b1, ucy | (uint32_t)(r1 >> 32) | (uint32_t)(b1 >> 32), bm, m1,
+    ((EXACT && SDK_SOLVE4_EXACT_UPD) ? upd4x : upd4)(c.x1, c.s1, ucx | (uint32_t)r1 | (uint32_t)b1, ucy | (uint32_t)(r1 >> 32) | (uint32_t)(b1 >> 32), bm, m1,
          chg);
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r2), "+v"(b2), "+v"(c.x1), "+v"(c.s1)::"memory");
-    upd4(c.x2, c.s2, ucx | (uint32_t)r2 | (uint32_t)b2, ucy | (uint32_t)(r2 >> 32) | (uint32_t)(b2 >> 32), bm, m2,
+    ((EXACT && SDK_SOLVE4_EXACT_UPD) ? upd4x : upd4)(c.x2, c.s2, ucx | (uint32_t)r2 | (uint32_t)b2, ucy | (uint32_t)(r2 >> 32) | (uint32_t)(b2 >> 32), bm, m2,
          chg);
 #else
     const uint2 uc = w.s_unit[w.ucol];
@@ -883,7 +949,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
 #endif
     while ((A0 | A1) != 0) {
         uint32_t bm, zmin, chg;
-        PROF4(0, round4(w, c, bm, zmin, chg));
+        // every board of the wave exact (an inactive slot is not): the shorter round
+        if (a.locked && __builtin_amdgcn_ballot_w64(c.E != kC2) == 0)
+            PROF4(0, round4<true>(w, c, bm, zmin, chg));
+        else
+            PROF4(0, round4<false>(w, c, bm, zmin, chg));
         ++a.iter;
         const uint32_t badw = bm | z16(zmin);
         const uint64_t B0 = spread_halves(__builtin_amdgcn_ballot_w64((badw & 0xFFFFu) != 0u));

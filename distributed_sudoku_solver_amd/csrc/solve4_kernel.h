@@ -265,12 +265,15 @@ __device__ __forceinline__ void upd4(uint32_t& X, uint32_t& S, uint32_t U, uint3
     X = xn;
 }
 
-// upd4 for waves whose boards are all exact (see unit4x): no "two hidden singles" test.
+// upd4 for waves whose boards are all exact (see unit4x): no "two hidden singles" test and
+// no empty-cell test (an open cell with no candidate left closes with S = 0: its units then
+// miss a digit, which the missing-digit test reports at the latest in the round that finds
+// the board complete).
 // Such a cell keeps both digits as candidates, each the only place of its digit in some
 // unit; every completion then misses one of them, so the missing-digit test refutes each
 // branch on it -- only later, in states that are contradictory anyway.
 __device__ __forceinline__ void upd4x(uint32_t& X, uint32_t& S, uint32_t U, uint32_t H, uint32_t& bm, uint32_t& m,
-                                     uint32_t& chg) {
+                                      uint32_t& chg) {
     uint32_t xn, v1, h, t, v2;
     asm("v_bitop3_b32 %[v1], %[x], %[u], %[u] bitop3:0x30\n\t"
         "v_and_b32 %[h], %[v1], %[hh]\n\t"
@@ -279,16 +282,16 @@ __device__ __forceinline__ void upd4x(uint32_t& X, uint32_t& S, uint32_t U, uint
         "v_bitop3_b32 %[v2], %[h], %[v1], %[t] bitop3:0xf4\n\t"
         "v_pk_add_u16 %[t], %[v2], -1\n\t"
         "v_and_b32 %[t], %[v2], %[t]\n\t"
-        "v_or_b32 %[m], %[v2], %[s]\n\t"
         "v_pk_add_u16 %[t], %[t], -1\n\t"
         "v_pk_ashrrev_i16 %[t], 15, %[t] op_sel_hi:[0,1]\n\t"
         "v_and_or_b32 %[s], %[v2], %[t], %[s]\n\t"
         "v_bitop3_b32 %[xn], %[v2], %[t], %[t] bitop3:0x30\n\t"
         "v_bitop3_b32 %[chg], %[chg], %[x], %[xn] bitop3:0xf6"
-        : [xn] "=&v"(xn), [v1] "=&v"(v1), [h] "=&v"(h), [t] "=&v"(t), [v2] "=&v"(v2), [m] "=&v"(m),
+        : [xn] "=&v"(xn), [v1] "=&v"(v1), [h] "=&v"(h), [t] "=&v"(t), [v2] "=&v"(v2),
           [s] "+v"(S), [bm] "+v"(bm), [chg] "+v"(chg)
         : [x] "v"(X), [u] "v"(U), [hh] "v"(H));
     X = xn;
+    m = 0x00010001u;   // no empty-cell test (see above)
 }
 
 // Unit summary of the lane's unit from its nine (X, S) cell words, one asm block.
@@ -440,7 +443,7 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
     upd4(c.x1, c.s1, uc.x | r1.x | b1.x, uc.y | r1.y | b1.y, bm, m1, chg);
     upd4(c.x2, c.s2, uc.x | r2.x | b2.x, uc.y | r2.y | b2.y, bm, m2, chg);
 #endif
-    zmin = min16(min16(m0, m1), m2);
+    zmin = EXACT ? 0x00010001u : min16(min16(m0, m1), m2);   // non-zero halves: no empty cell
 }
 
 // per-slot search state, uniform within the half.  It lives in LDS between steps

@@ -386,9 +386,10 @@ __device__ __forceinline__ void unit4x(const uint2 (&v)[9], uint32_t E, uint32_t
 }
 
 // One propagation round for all four boards, branch-free.  Out: per-lane packed
-// contradiction bits (bm, zmin) and change bits (chg).
+// contradiction bits (bad: non-zero in a half = that board is contradictory) and change
+// bits (chg).
 template <bool EXACT>
-__device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, uint32_t& zmin, uint32_t& chg) {
+__device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bad, uint32_t& chg) {
     w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
     w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
     w.s_cell[w.c0 + 54] = make_uint2(c.x2, c.s2);
@@ -396,7 +397,7 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
     uint2 v[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) v[k] = w.s_cell[w.ucell[k]];
-    uint32_t once, T;
+    uint32_t once, T, bm;
     if (EXACT)
         unit4x(v, c.E, once, T, bm);
     else
@@ -443,7 +444,9 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bm, 
     upd4(c.x1, c.s1, uc.x | r1.x | b1.x, uc.y | r1.y | b1.y, bm, m1, chg);
     upd4(c.x2, c.s2, uc.x | r2.x | b2.x, uc.y | r2.y | b2.y, bm, m2, chg);
 #endif
-    zmin = EXACT ? 0x00010001u : min16(min16(m0, m1), m2);   // non-zero halves: no empty cell
+    // an open cell without candidates (a zero half of m0..m2); exact waves leave it to the
+    // missing-digit test (upd4x)
+    bad = EXACT ? bm : bm | z16(min16(min16(m0, m1), m2));
 }
 
 // per-slot search state, uniform within the half.  It lives in LDS between steps
@@ -951,14 +954,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     const uint64_t tl_ = __builtin_amdgcn_s_memtime();
 #endif
     while ((A0 | A1) != 0) {
-        uint32_t bm, zmin, chg;
+        uint32_t badw, chg;
         // every board of the wave exact (an inactive slot is not): the shorter round
         if (a.locked && __builtin_amdgcn_ballot_w64(c.E != kC2) == 0)
-            PROF4(0, round4<true>(w, c, bm, zmin, chg));
+            PROF4(0, round4<true>(w, c, badw, chg));
         else
-            PROF4(0, round4<false>(w, c, bm, zmin, chg));
+            PROF4(0, round4<false>(w, c, badw, chg));
         ++a.iter;
-        const uint32_t badw = bm | z16(zmin);
         const uint64_t B0 = spread_halves(__builtin_amdgcn_ballot_w64((badw & 0xFFFFu) != 0u));
         const uint64_t B1 = spread_halves(__builtin_amdgcn_ballot_w64(badw > 0xFFFFu));
         const uint64_t C0 = spread_halves(__builtin_amdgcn_ballot_w64((chg & 0xFFFFu) != 0u));

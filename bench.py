@@ -642,6 +642,15 @@ def main():
     dog.daemon = True
     dog.start()
 
+    def side(name, fn):
+        # a side leg that raises (e.g. a collective refused on some node) is recorded, not fatal:
+        # the headline line above is measured and still printed
+        try:
+            result[name] = fn()
+        except Exception as e:  # noqa: BLE001
+            result[name] = {"error": f"{type(e).__name__}: {e}"}
+        return result[name]
+
     # ------------------------------------------------ weak-scaling figure
     if d.world > 1 and args.weak_leg:
         wp, we = gen(total, seed=args.seed, lo=d.rank * total)
@@ -656,12 +665,12 @@ def main():
 
     # ------------------------------------------------------------ C2 leg
     if args.c2_puzzles > 0:
-        result["c2_30clue"] = c2_leg(eng, d, args, synth)
+        side("c2_30clue", lambda: c2_leg(eng, d, args, synth))
 
     # ------------------------------------------------ distinct minimal puzzles
     if args.minimal_puzzles > 0:
-        result["minimal_puzzles"] = minimal_leg(eng, d, args, synth, L)
-        bad_total += result["minimal_puzzles"]["parity"]["mismatched_boards"]
+        leg = side("minimal_puzzles", lambda: minimal_leg(eng, d, args, synth, L))
+        bad_total += leg.get("parity", {}).get("mismatched_boards", 0)
 
     # ------------------------------------------------------------ C5 leg
     if args.count_leg and getattr(args, "shared_gpus", False):
@@ -669,8 +678,8 @@ def main():
         # GPUs has no C5 leg (on a node every rank has its own GPU)
         result["c5_count"] = {"skipped": "more ranks than GPUs: RCCL needs one device per rank"}
     elif args.count_leg:
-        result["c5_count"] = c5_leg(eng, d, synth)
-        result["c5_count_rebalanced"] = c5_rebalanced_leg(eng, d, synth)
+        side("c5_count", lambda: c5_leg(eng, d, synth))
+        side("c5_count_rebalanced", lambda: c5_rebalanced_leg(eng, d, synth))
 
     # ---------------------------------------------------------- CPU baseline
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
@@ -681,12 +690,12 @@ def main():
         result["cpu_baseline_c_port"] = cpu_baseline_c(puzzles, args.cpu_seconds, cores)
 
     if d.rank == 0 and d.world == 1 and args.http_requests > 0:
-        result["post_solve_latency"] = http_leg(args.http_requests)
+        side("post_solve_latency", lambda: http_leg(args.http_requests))
 
     # -------------------------------------------- per-lane reference DFS (north star part 3)
     if d.rank == 0 and d.world == 1 and args.lane_puzzles > 0:
-        result["lane_dfs"] = lane_dfs_leg(eng, args, synth, L)
-        bad_total += result["lane_dfs"]["parity"]["mismatched_boards"]
+        leg = side("lane_dfs", lambda: lane_dfs_leg(eng, args, synth, L))
+        bad_total += leg.get("parity", {}).get("mismatched_boards", 0)
 
     dog.cancel()
     eng.close()

@@ -5,8 +5,9 @@ Headline (BASELINE.json metric): 17-clue hard puzzles solved per second, whole
 job, config C4 = 10M transformed 17-clue puzzles SHARDED over the N GPUs (rank k
 owns rows [k*10M/N, (k+1)*10M/N) of one seeded stream, resident in HBM; strong
 scaling); one "step" = one sdk_solve_batch_dev pass of every rank over its
-slice.  No collective on the data path; torch.distributed (gloo) carries only
-the barrier and the max-over-ranks time.  After timing, every solved board is
+slice.  No collective on the data path; the ranks' barrier and max-over-ranks
+time go over hostcomm.TcpComm (standard-library sockets: the product's own host
+transport -- nothing here imports torch).  After timing, every solved board is
 compared with its expected solution (known by construction) -- a mismatch fails
 the run.  At N > 1 a secondary weak-scaling figure (10M puzzles per GPU) is
 reported beside it.
@@ -78,6 +79,11 @@ def parse_args():
     ap.add_argument("--minimal-puzzles", type=int, default=1 << 20,
                     help="distinct minimal-puzzle leg, puzzles per GPU (0 = skip)")
     ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
+    ap.add_argument("--c5-boards", default="15,14",
+                    help="C5 boards: 16/15/14 clues (S1 with clues removed; counts 7,309 / 3,481,026 / 18,204,270); "
+                         "the first is counted by the two-stage split, the second by the rebalanced one")
+    ap.add_argument("--frontier-probe", type=int, default=1_000_000,
+                    help="boards of the timed one-board frontier build beside the rebalanced count (0 = skip)")
     ap.add_argument("--lane-puzzles", type=int, default=200_000,
                     help="per-lane reference-DFS leg on a C2 prefix (rank 0, N=1; 0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
@@ -90,50 +96,40 @@ def parse_args():
 
 
 class Dist:
+    """The ranks' host exchanges (barrier, max/sum of one number) over hostcomm.TcpComm: the
+    product's own standard-library transport, the one that also hands out the RCCL id of the C5
+    legs.  Ranks come from RANK / WORLD_SIZE / LOCAL_RANK (torchrun or launch_ranks), the
+    rendezvous from MASTER_ADDR and SDK_RDZV_PORT (else MASTER_PORT + 1)."""
+
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
+        self.comm = None
         if self.world > 1:
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            # gloo prints its connection log on the process's stdout; rank 0's stdout must be
-            # exactly the one JSON line, so fd 1 points at stderr while the group forms
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-            finally:
-                sys.stdout.flush()
-                os.dup2(saved, 1)
-                os.close(saved)
-            self.dist = dist
+            from distributed_sudoku_solver_amd.hostcomm import TcpComm
+            self.comm = TcpComm(self.rank, self.world, addr=os.environ.get("MASTER_ADDR", "127.0.0.1"))
 
     def barrier(self):
         if self.world > 1:
-            self.dist.barrier()
+            self.comm.barrier()
+
+    def _reduce(self, x, op):
+        if self.world == 1:
+            return x
+        buf = np.array([float(x)], dtype=np.float64)
+        self.comm.allreduce(buf, 1, np.float64, op)
+        return float(buf[0])
 
     def max(self, x):
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return self._reduce(x, "max")
 
     def sum(self, x):
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return self._reduce(x, "sum")
 
     def close(self):
-        if self.world > 1:
-            self.dist.destroy_process_group()
+        if self.comm is not None:
+            self.comm.close()
 
 
 def pmc_record(path, kernel, units):
@@ -256,14 +252,26 @@ def c2_leg(eng, d, args, synth):
 
 
 C5_BOARD_SOLUTIONS = 3_481_026    # S1 with its last row cleared (15 clues)
+C5_14CLUE_SOLUTIONS = 18_204_270   # SURVEY §8(d) C5: the 15-clue board minus one more clue (C probe)
 
 
-def c5_leg(eng, d, synth):
+def c5_board(synth, clues):
+    """SURVEY §8(d) C5 boards: S1 with clues removed -> (board, expected count, description)."""
+    b15 = synth.SEEDS17["S1"][:-9] + "0" * 9
+    spec = {"16": (synth.SEEDS17["S1"][:-9] + "000800000", 7_309, "S1 minus its last row but one clue (16 clues)"),
+            "15": (b15, C5_BOARD_SOLUTIONS, "S1 minus its last row (15 clues)"),
+            "14": (b15[:63] + "000100000" + "0" * 9, C5_14CLUE_SOLUTIONS,
+                   "S1 minus its last row and one more clue (14 clues)")}[str(clues)]
+    return synth.parse(spec[0]), spec[1], spec[2]
+
+
+def c5_leg(eng, d, args, synth):
     """Config C5: exhaustive count of one 15-clue board.  Every rank expands the same frontier
-    and counts its interleaved share; one RCCL all-reduce (device memory, xGMI) combines them."""
-    from distributed_sudoku_solver_amd.shard import HostComm, RcclComm, sharded_count
-    board = synth.parse(synth.SEEDS17["S1"][:-9] + "0" * 9)
-    comm = RcclComm(eng, d.rank, d.world, transport=HostComm(d.rank, d.world)) if d.world > 1 else None
+    and counts its interleaved share; one RCCL all-reduce (device memory, xGMI) combines them.
+    The RCCL id travels over the ranks' TcpComm."""
+    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count
+    board, expected, what = c5_board(synth, args.c5_boards.split(",")[0])
+    comm = RcclComm(eng, d.rank, d.world, transport=d.comm) if d.world > 1 else None
     try:
         sharded_count(eng, board, d.rank, d.world, comm=comm)            # warm-up
         walls = []
@@ -276,23 +284,20 @@ def c5_leg(eng, d, synth):
         if comm is not None:
             comm.close()
     w = min(walls)
-    return {"workload": "C5: count every completion of S1 minus its last row (15 clues), frontier split over "
+    return {"workload": f"C5: count every completion of {what}, frontier split over "
                         f"{d.world} GPU(s)" + (", RCCL all-reduce" if d.world > 1 else ""),
-            "solutions": total, "expected": C5_BOARD_SOLUTIONS, "ok": total == C5_BOARD_SOLUTIONS and st == 1,
+            "solutions": total, "expected": expected, "ok": total == expected and st == 1,
             "frontier_boards": size, "wall_ms": w * 1000.0, "value": total / w, "unit": "solutions/s"}
 
 
-C5_14CLUE_SOLUTIONS = 18_204_270   # SURVEY §8(d) C5: the 15-clue board minus one more clue (C probe)
-
-
-def c5_rebalanced_leg(eng, d, synth):
+def c5_rebalanced_leg(eng, d, args, synth):
     """Config C5 on the 14-clue board with dynamic rebalancing: ranks start on equal blocks of the
     replicated frontier and, after every round, all-gather their live ranges over RCCL (xGMI) so dry
     ranks take half of the largest remaining one (shard.sharded_count_rebalanced)."""
-    from distributed_sudoku_solver_amd.shard import HostComm, RcclComm, sharded_count_rebalanced
-    b15 = synth.SEEDS17["S1"][:-9] + "0" * 9
-    board = synth.parse(b15[:63] + "000100000" + "0" * 9)
-    comm = RcclComm(eng, d.rank, d.world, transport=HostComm(d.rank, d.world)) if d.world > 1 else None
+    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_count_rebalanced
+    specs = args.c5_boards.split(",")
+    board, expected, what = c5_board(synth, specs[1] if len(specs) > 1 else specs[0])
+    comm = RcclComm(eng, d.rank, d.world, transport=d.comm) if d.world > 1 else None
     try:
         sharded_count_rebalanced(eng, board, d.rank, d.world, comm=comm)   # warm-up
         walls = []
@@ -308,19 +313,19 @@ def c5_rebalanced_leg(eng, d, synth):
     w = min(walls)
     # frontier scale: a ~1M-board frontier of the same board (tile scan over the chip,
     # device-side level loop), timed alone
-    fw = []
-    for _ in range(3):
-        eng.synchronize()
-        t0 = time.perf_counter()
-        fsize, _ = eng.frontier_build(board, target=1_000_000)
-        fw.append(time.perf_counter() - t0)
-    info["frontier_1m"] = {"boards": fsize, "build_ms": 1000 * min(fw)}
+    if args.frontier_probe > 0:
+        fw = []
+        for _ in range(3):
+            eng.synchronize()
+            t0 = time.perf_counter()
+            fsize, _ = eng.frontier_build(board, target=args.frontier_probe)
+            fw.append(time.perf_counter() - t0)
+        info["frontier_1m"] = {"boards": fsize, "build_ms": 1000 * min(fw)}
     return {"frontier_1m": info.get("frontier_1m"),
-            "workload": "C5: count every completion of a 14-clue board (S1, last row cleared, one more clue "
-                        f"removed), rebalanced frontier over {d.world} GPU(s)"
+            "workload": f"C5: count every completion of {what}, rebalanced frontier over {d.world} GPU(s)"
                         + (", RCCL all-gather of live ranges + all-reduce" if d.world > 1 else ""),
-            "solutions": total, "expected": C5_14CLUE_SOLUTIONS,
-            "ok": total == C5_14CLUE_SOLUTIONS and st == 1, "frontier_boards": size,
+            "solutions": total, "expected": expected,
+            "ok": total == expected and st == 1, "frontier_boards": size,
             "rounds": info.get("rounds"), "steals": info.get("steals"),
             "wall_ms": w * 1000.0, "value": total / w, "unit": "solutions/s"}
 
@@ -435,13 +440,20 @@ def launch_ranks(args):
     the torchrun environment, before this process touches any GPU; rank 0 prints the line."""
     import socket
     import subprocess
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
+    ports = []
+    socks = [socket.socket() for _ in range(2)]
+    try:
+        for sk in socks:
+            sk.bind(("127.0.0.1", 0))
+            ports.append(sk.getsockname()[1])
+    finally:
+        for sk in socks:
+            sk.close()
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
-                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(ports[0]),
+                   SDK_RDZV_PORT=str(ports[1]))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
     codes = [p.wait() for p in procs]
@@ -678,8 +690,8 @@ def main():
         # GPUs has no C5 leg (on a node every rank has its own GPU)
         result["c5_count"] = {"skipped": "more ranks than GPUs: RCCL needs one device per rank"}
     elif args.count_leg:
-        side("c5_count", lambda: c5_leg(eng, d, synth))
-        side("c5_count_rebalanced", lambda: c5_rebalanced_leg(eng, d, synth))
+        side("c5_count", lambda: c5_leg(eng, d, args, synth))
+        side("c5_count_rebalanced", lambda: c5_rebalanced_leg(eng, d, args, synth))
 
     # ---------------------------------------------------------- CPU baseline
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:

@@ -20,6 +20,7 @@ SDK_ECOMM = -4
 SDK_SOLVED = 1
 SDK_UNSOLVABLE = 0
 SDK_BUDGET_HIT = -2
+SDK_BUDGET_CONTEXT = (1 << 64) - 1    # sdk_solve_batch_budget: use the context's SDK_OPT_NODE_BUDGET
 
 SDK_CHECK_OK = 1
 SDK_CHECK_RAW_NAMEERROR = 2
@@ -81,6 +82,9 @@ SIGNATURES = {
     "sdk_check_batch": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
     "sdk_check_batch_i64": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
     "sdk_solve_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz]),
+    "sdk_solve_batch_budget": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint64]),
+    "sdk_expand_boards": (ctypes.c_int, [_vp, _vp, _vp, _sz, ctypes.c_uint64, _vp, _sz,
+                                         ctypes.POINTER(ctypes.c_uint64)]),
     "sdk_count_solutions": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.POINTER(ctypes.c_int8)]),
     "sdk_count_solutions_slice": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,

@@ -38,7 +38,9 @@ namespace sdk {
 // device-side control block of one frontier build
 struct FrontierCtl {
     unsigned long long m;        // boards in the current frontier
-    unsigned long long leaves;   // completions met while expanding (count mode), cumulative
+    unsigned long long leaves;   // completions met while expanding (count mode), accepted levels only
+    unsigned long long lvl_leaves;  // completions met by the level being expanded (folded into
+                                    // `leaves` by frontier_end_kernel only if the level is accepted)
     unsigned long long open;     // boards that branched in the current level
     unsigned long long total;    // children of the current level (scan)
     unsigned int level;          // completed levels: the frontier is in buffer (level & 1)
@@ -80,13 +82,16 @@ __global__ void frontier_begin_kernel(FrontierCtl* ctl, uint64_t target, int for
     }
     ctl->next = 0;
     ctl->open = 0;
+    ctl->lvl_leaves = 0;
 }
 
 // level end: the children become the frontier; first-solution mode stops when nothing
 // branched (the next level would equal this one)
 __global__ void frontier_end_kernel(FrontierCtl* ctl, int first) {
-    if (ctl->done) return;
+    if (ctl->done) return;   // also a level that scan_top_kernel rejected: its leaves are dropped, its
+                             // parents (which contain them) stay the frontier
     ctl->m = ctl->total;
+    ctl->leaves += ctl->lvl_leaves;
     ctl->level += 1;
     if (ctl->total == 0 || (first && ctl->open == 0)) ctl->done = 1;
 }
@@ -134,7 +139,7 @@ __global__ __launch_bounds__(64) void expand_kernel(ExpandArgs a) {
                     dst[lane] = (uint8_t)board_byte(inA, sa);
                     if (w.hasB) dst[64 + lane] = (uint8_t)board_byte(inB, sb);
                 } else if (lane == 0) {
-                    atomicAdd(&a.ctl->leaves, 1ull);
+                    atomicAdd(&a.ctl->lvl_leaves, 1ull);
                 }
             } else if (r == P_OPEN) {
                 if (lane == 0) atomicAdd(&a.ctl->open, 1ull);

@@ -114,7 +114,7 @@ int ensure(DevBuf& b, size_t bytes) {
 int timer_begin(sdk_ctx* c, hipEvent_t* stop_out) {
     *stop_out = nullptr;
     if (!c->timing) return SDK_OK;
-    if (c->events_used >= kMaxTimedLaunches) return fail(SDK_EINVAL, "%d timed launches since sdk_timer_reset", kMaxTimedLaunches);
+    if (c->events_used >= kMaxTimedLaunches) return fail(SDK_EINVAL, "%zu timed launches since sdk_timer_reset", kMaxTimedLaunches);
     if (c->events_used == c->events.size()) {
         hipEvent_t a, b;
         HIPCALL(hipEventCreate(&a));
@@ -157,7 +157,9 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
 int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
                  uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
                  unsigned long long* d_counts = nullptr, uint64_t in_first = 0, uint64_t in_step = 1,
-                 int order = -1) {
+                 int order = -1, int64_t budget = -1) {
+    // budget: node budget per board for this launch (-1 = the context's SDK_OPT_NODE_BUDGET)
+    const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
     if (n == 0) return SDK_OK;
     if (n > 0x7FFFFFFFull) return fail(SDK_EINVAL, "at most 2^31-1 boards per call");
     if (c->solver == SDK_SOLVER_LANE && !count_mode) {
@@ -177,7 +179,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
         a.work = d_work;
         a.n = n;
         a.next = static_cast<uint32_t*>(c->counter.p);
-        a.budget = c->budget;
+        a.budget = node_budget;
         a.in_first = in_first;
         a.in_step = in_step;
         const uint64_t blocks = (n + sdk::kLaneThreads - 1) / sdk::kLaneThreads;
@@ -225,7 +227,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.n = n;
     a.next = static_cast<uint32_t*>(c->counter.p);
     a.stack = static_cast<uint32_t*>(c->stack.p);
-    a.budget = c->budget;
+    a.budget = node_budget;
     a.order = order >= 0 ? order : c->order;
     a.limit = limit;
     a.count = d_count;
@@ -280,7 +282,10 @@ uint64_t frontier_capacity(uint64_t m0, uint64_t target) {
 
 // The caller has put the m0 boards in fr_a, sized for frontier_capacity(m0, target) boards
 // BEFORE seeding it (a later grow would drop them).
-int run_frontier_levels(sdk_ctx* c, uint64_t m0, bool use_mask, int mode, uint64_t target) {
+// use_mask: fr_mask holds one first-cell mask per seed board (level 0 applies them);
+// force0: level 0 is expanded whatever the seed count (a seed board's mask lives only in that
+// level, and sdk_expand_boards always wants at least one level).
+int run_frontier_levels(sdk_ctx* c, uint64_t m0, bool use_mask, int mode, uint64_t target, bool force0) {
     int rc;
     const bool first = mode == SDK_FRONTIER_FIRST;
     const uint64_t m_exp = std::max<uint64_t>(m0, std::min(target, kFrontierCap));
@@ -306,7 +311,7 @@ int run_frontier_levels(sdk_ctx* c, uint64_t m0, bool use_mask, int mode, uint64
     constexpr int kLevelsPerSync = 4;
     for (int level = 0; level < 81; ++level) {
         const int in = level & 1;
-        sdk::frontier_begin_kernel<<<1, 1, 0, c->stream>>>(ctl, target, level == 0 && use_mask ? 1 : 0);
+        sdk::frontier_begin_kernel<<<1, 1, 0, c->stream>>>(ctl, target, level == 0 && force0 ? 1 : 0);
         sdk::ExpandArgs ea;
         ea.in = static_cast<const uint8_t*>(buf[in]);
         ea.ctl = ctl;
@@ -351,7 +356,7 @@ int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, i
     if ((rc = ensure(c->fr_a, frontier_capacity(1, target) * 81)) || (rc = ensure(c->fr_mask, 16))) return rc;
     HIPCALL(hipMemcpyAsync(c->fr_a.p, h_board, 81, hipMemcpyHostToDevice, c->stream));
     if (h_mask) HIPCALL(hipMemcpyAsync(c->fr_mask.p, h_mask, 2, hipMemcpyHostToDevice, c->stream));
-    return run_frontier_levels(c, 1, h_mask != nullptr, mode, target);
+    return run_frontier_levels(c, 1, h_mask != nullptr, mode, target, h_mask != nullptr);
 }
 
 // Keep frontier boards first, first+step, ... of the current (count-mode) frontier and
@@ -382,7 +387,32 @@ int refine_frontier(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t target) 
         c->fr_valid = true;
         return SDK_OK;
     }
-    return run_frontier_levels(c, n, false, SDK_FRONTIER_COUNT, target);
+    return run_frontier_levels(c, n, false, SDK_FRONTIER_COUNT, target, false);
+}
+
+// Lex-ordered (SDK_FRONTIER_FIRST) breadth-first expansion of n seed boards, each with its own
+// first-cell mask, at least one level deep and on until the frontier holds >= target boards;
+// the frontier is copied to the host.  Children keep their parents' order, so the result is
+// sorted by the completions below each board (see frontier_kernel.h): the worklist step of a
+// resumable lex-first search (search.py), which expands the boards that hit the node budget.
+int expand_boards(sdk_ctx* c, const uint8_t* h_in, const uint16_t* h_masks, uint64_t n, uint64_t target,
+                  uint8_t* h_out, uint64_t cap, uint64_t* out_n) {
+    c->fr_valid = false;
+    *out_n = 0;
+    if (n == 0) return SDK_OK;
+    if (n > kFrontierCap) return fail(SDK_EINVAL, "at most %llu seed boards", (unsigned long long)kFrontierCap);
+    int rc;
+    if ((rc = ensure(c->fr_a, frontier_capacity(n, target) * 81)) || (rc = ensure(c->fr_mask, n * 2))) return rc;
+    HIPCALL(hipMemcpyAsync(c->fr_a.p, h_in, n * 81, hipMemcpyHostToDevice, c->stream));
+    if (h_masks) HIPCALL(hipMemcpyAsync(c->fr_mask.p, h_masks, n * 2, hipMemcpyHostToDevice, c->stream));
+    if ((rc = run_frontier_levels(c, n, h_masks != nullptr, SDK_FRONTIER_FIRST, target, true))) return rc;
+    if (c->fr_size > cap)
+        return fail(SDK_EINVAL, "frontier of %llu boards exceeds cap %llu (pass cap >= 9 * max(n, target))",
+                    (unsigned long long)c->fr_size, (unsigned long long)cap);
+    if (c->fr_size) HIPCALL(hipMemcpyAsync(h_out, c->fr_a.p, c->fr_size * 81, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    *out_n = c->fr_size;
+    return SDK_OK;
 }
 
 // Count the completions below frontier boards first, first+step, ... < end into
@@ -726,7 +756,14 @@ int sdk_check_batch_i64(sdk_ctx* c, const int64_t* boards, uint8_t* verdict, siz
 
 int sdk_solve_batch(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell_mask, uint8_t* out, int8_t* status,
                     uint64_t* work, size_t n) {
+    return sdk_solve_batch_budget(c, in, first_cell_mask, out, status, work, n, SDK_BUDGET_CONTEXT);
+}
+
+int sdk_solve_batch_budget(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell_mask, uint8_t* out,
+                           int8_t* status, uint64_t* work, size_t n, uint64_t node_budget) {
     if (!c || (n && (!in || !out || !status))) return fail(SDK_EINVAL, "NULL argument");
+    if (node_budget != SDK_BUDGET_CONTEXT && node_budget > (uint64_t)INT64_MAX)
+        return fail(SDK_EINVAL, "node budget out of range");
     if (n == 0) return SDK_OK;
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
@@ -738,7 +775,8 @@ int sdk_solve_batch(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell_ma
     if (first_cell_mask) HIPCALL(hipMemcpyAsync(c->mask.p, first_cell_mask, n * 2, hipMemcpyHostToDevice, c->stream));
     rc = launch_solve(c, static_cast<uint8_t*>(c->in.p), first_cell_mask ? static_cast<uint16_t*>(c->mask.p) : nullptr,
                       static_cast<uint8_t*>(c->out.p), static_cast<int8_t*>(c->status.p),
-                      work ? static_cast<uint64_t*>(c->work.p) : nullptr, n, 0, 0, nullptr);
+                      work ? static_cast<uint64_t*>(c->work.p) : nullptr, n, 0, 0, nullptr, nullptr, 0, 1, -1,
+                      node_budget == SDK_BUDGET_CONTEXT ? -1 : (int64_t)node_budget);
     if (rc) return rc;
     HIPCALL(hipMemcpyAsync(out, c->out.p, n * 81, hipMemcpyDeviceToHost, c->stream));
     HIPCALL(hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
@@ -773,6 +811,14 @@ int sdk_frontier_build(sdk_ctx* c, const uint8_t* board, const uint16_t* first_c
     if (size) *size = c->fr_size;
     if (leaves) *leaves = c->fr_leaves;
     return SDK_OK;
+}
+
+int sdk_expand_boards(sdk_ctx* c, const uint8_t* boards, const uint16_t* first_cell_masks, size_t n,
+                      uint64_t target, uint8_t* out, size_t cap, uint64_t* out_n) {
+    if (!c || !out_n || (n && (!boards || !out))) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    return expand_boards(c, boards, first_cell_masks, n, target, out, cap, out_n);
 }
 
 int sdk_frontier_refine(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t target, uint64_t* size,

@@ -211,8 +211,11 @@ class SudokuEngine:
         L.check(fn(self.ctx, _ptr(boards), _ptr(verdict), n), "sdk_check_batch_i64" if wide else "sdk_check_batch")
         return verdict
 
-    def solve_batch(self, boards, masks=None, want_work=False):
-        """uint8[n,81] (+ optional uint16[n] first-cell masks) -> (out uint8[n,81], status int8[n], work)."""
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
+        """uint8[n,81] (+ optional uint16[n] first-cell masks) -> (out uint8[n,81], status int8[n], work).
+
+        budget: search nodes per board for this call (sdk_solve_batch_budget; 0 = unlimited),
+        None = the context's SDK_OPT_NODE_BUDGET.  A board that runs out is SDK_BUDGET_HIT."""
         boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
         n = boards.shape[0]
         if masks is not None:
@@ -220,9 +223,30 @@ class SudokuEngine:
         out = np.empty_like(boards)
         status = np.empty(n, dtype=np.int8)
         work = np.empty(n, dtype=np.uint64) if want_work else None
-        L.check(self.lib.sdk_solve_batch(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status),
-                                         _ptr(work), n), "sdk_solve_batch")
+        if budget is None:
+            L.check(self.lib.sdk_solve_batch(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status),
+                                             _ptr(work), n), "sdk_solve_batch")
+        else:
+            if not 0 <= int(budget) < (1 << 63):
+                raise ValueError("budget must be 0 (unlimited) or a positive node count")
+            L.check(self.lib.sdk_solve_batch_budget(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status),
+                                                    _ptr(work), n, int(budget)), "sdk_solve_batch_budget")
         return out, status, work
+
+    def expand(self, boards, masks=None, target=64):
+        """Lex-ordered frontier below `boards` (sdk_expand_boards): uint8[k,81], children in the
+        reference's DFS order, parents' order kept; at least one level, >= target boards unless
+        nothing branches.  Contradicted subtrees vanish, solved boards stay."""
+        boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
+        n = boards.shape[0]
+        if masks is not None:
+            masks = np.ascontiguousarray(masks, dtype=np.uint16).reshape(n)
+        cap = 9 * max(n, int(target), 1)
+        out = np.empty((cap, 81), dtype=np.uint8)
+        k = ctypes.c_uint64()
+        L.check(self.lib.sdk_expand_boards(self.ctx, _ptr(boards), _ptr(masks), n, int(target), _ptr(out), cap,
+                                           ctypes.byref(k)), "sdk_expand_boards")
+        return out[:k.value].copy()
 
     def count_solutions(self, board, limit=0):
         board = np.ascontiguousarray(board, dtype=np.uint8).reshape(81)

@@ -52,11 +52,15 @@ def default_port():
 
 
 class TcpComm:
-    """Star transport: rank 0 listens on (addr, port), ranks 1..world-1 connect."""
+    """Star transport: rank 0 listens on (addr, port), ranks 1..world-1 connect.
+
+    `timeout` bounds the rendezvous only (connect / accept / the rank handshake); once
+    connected the sockets block without a limit (`data_timeout`, default None): a rank may
+    wait as long as a peer's shard takes (hard boards, the per-lane solver)."""
 
     _OPS = {"sum": np.sum, "min": np.min, "max": np.max}
 
-    def __init__(self, rank, world, addr=None, port=None, timeout=120.0):
+    def __init__(self, rank, world, addr=None, port=None, timeout=120.0, data_timeout=None):
         if world < 1 or not 0 <= rank < world:
             raise ValueError(f"bad rank {rank} / world {world}")
         self.rank, self.world = rank, world
@@ -82,6 +86,8 @@ class TcpComm:
                     self.peers[r] = conn
             finally:
                 srv.close()
+            for conn in self.peers.values():
+                conn.settimeout(data_timeout)
         else:
             while True:
                 try:
@@ -94,6 +100,7 @@ class TcpComm:
             s.settimeout(timeout)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             s.sendall(struct.pack("<i", rank))
+            s.settimeout(data_timeout)
             self.sock = s
 
     # ----------------------------------------------------------- byte level
@@ -185,3 +192,9 @@ class TcpComm:
                 pass
         self.peers = {}
         self.sock = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

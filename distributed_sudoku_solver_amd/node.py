@@ -38,6 +38,18 @@ What changes (GPU-first):
   * api="main" serves main.py's HTTP surface instead (main.py:356-406): POST
     /solve -> 201 {"solution"}; GET /stats (local counters only); GET /network
     -> {"node": "h:p", "predecessor": [h, p] | null, "neighbor": [h, p] | null}.
+  * Every launch is bounded (SURVEY §7 hard parts 2 and 7): a batch gives each
+    board `node_budget` search nodes (sdk_solve_batch_budget), so one hard board
+    cannot hold back the others; a board that hits it is continued alone by a
+    search.LexSearch in slices of one bounded launch each, which the worker
+    interleaves with new batches (the node keeps answering POSTs, /stats and
+    the ring).  A budget hit is never reported as NO_SOLUTION: the range stays
+    open.  If the continued search gives up (`search_limit_s`, or its worklist
+    outgrows search.DEFAULT_MAX_PENDING) the range is reported as EXHAUSTED {uuid,
+    range, sudoku} (a new method; reference nodes ignore it) and the HTTP origin
+    answers 504 {"solution": null, "exhausted": true, "error": ...} once no
+    completion below that range can still arrive -- never a completion that might
+    not be the lex-first one.
 """
 import argparse
 import collections
@@ -54,12 +66,43 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 import numpy as np
 
 from .engine import ALL_DIGITS_MASK, encode_solve_grid, range_to_mask
+from .search import DEFAULT_BUDGET, DEFAULT_MAX_PENDING, DEFAULT_WIDTH, LexSearch
 from .utils import split_array_in_middle
 from . import _lib as L
 
 RECV_BYTES = 1024          # DHT_Node.py:82,94
 HEARTBEAT_S = 5.0          # DHT_Node.py:43
 STATS_WAIT_S = 1.0         # DHT_Node.py:571
+SEARCH_LIMIT_S = 30.0      # a budget-hit task's continued search gives up after this (EXHAUSTED)
+DONE_UUIDS_KEPT = 1 << 16  # answered puzzles remembered (late duplicates are dropped)
+
+
+class _RecentSet:
+    """A set that forgets its oldest members beyond `cap` (the reference keeps no such
+    state at all; unbounded it would grow with every puzzle the ring ever solved)."""
+
+    def __init__(self, cap=DONE_UUIDS_KEPT):
+        self.cap = cap
+        self._d = collections.OrderedDict()
+
+    def add(self, x):
+        self._d[x] = None
+        self._d.move_to_end(x)
+        while len(self._d) > self.cap:
+            self._d.popitem(last=False)
+
+    def __contains__(self, x):
+        return x in self._d
+
+    def __len__(self):
+        return len(self._d)
+
+
+class _HardTask:
+    """A TASK whose launch hit the node budget, continued by a LexSearch between batches."""
+
+    def __init__(self, task, search, deadline):
+        self.task, self.search, self.deadline = task, search, deadline
 
 
 class _ProtocolUnpickler(pickle.Unpickler):
@@ -91,7 +134,8 @@ class SudokuNode:
 
     def __init__(self, host, p2p_port, http_port, anchor=None, engine=None, delay_ms=0.0,
                  heartbeat_s=HEARTBEAT_S, stats_wait_s=STATS_WAIT_S, solve_timeout_s=600.0, log=False,
-                 api="dht", split=True, trace=False):
+                 api="dht", split=True, trace=False, node_budget=DEFAULT_BUDGET, search_limit_s=SEARCH_LIMIT_S,
+                 search_width=DEFAULT_WIDTH, search_max_pending=DEFAULT_MAX_PENDING):
         if api not in ("dht", "main"):
             raise ValueError("api must be 'dht' (DHT_Node.py) or 'main' (main.py)")
         self.api = api
@@ -105,6 +149,12 @@ class SudokuNode:
         self.heartbeat_s = heartbeat_s
         self.stats_wait_s = stats_wait_s
         self.solve_timeout_s = solve_timeout_s
+        if node_budget < 1:
+            raise ValueError("node_budget must be >= 1: an unbounded launch can hold the GPU forever")
+        self.node_budget = int(node_budget)
+        self.search_limit_s = float(search_limit_s)
+        self.search_width = int(search_width)
+        self.search_max_pending = int(search_max_pending)
         self.log = log
         if engine is None:
             from .solver import default_engine
@@ -122,10 +172,11 @@ class SudokuNode:
         # work state
         self.tasks = queue.Queue()               # pending TASK dicts
         self.neighbor_tasks = []                 # tasks handed to the neighbour (re-run on its failure)
+        self.hard = []                           # _HardTask: budget-hit tasks continued between batches
         self.busy = False
-        self.done_uuids = set()                  # uuids already solved somewhere in the ring
-        self.best = {}                           # uuid -> (lowest digit, grid): best ordered completion so far
-        self.waiters = {}                        # uuid -> (Event, [solution], puzzle, failed digit mask)
+        self.done_uuids = _RecentSet()           # uuids already solved somewhere in the ring
+        self.best = {}                           # uuid -> (lowest digit, grid): best ordered completion (origin only)
+        self.waiters = {}                        # uuid -> (Event, [solution], puzzle, [failed mask, exhausted mask])
         self.trace = collections.deque(maxlen=4096) if trace else None   # (method, addr, range) sent
         self.validations = 0
         self.solved_count = 0
@@ -185,7 +236,8 @@ class SudokuNode:
         (DHT_Node.py:137-156); graceful=False simulates a crash."""
         if graceful and self.running:
             with self.lock:
-                pending = self._drain_queue()
+                pending = self._drain_queue() + [h.task for h in self.hard]
+                self.hard = []
                 if self.neighbor and self.neighbor != self.me:
                     for t in pending:
                         self.send(t, self.neighbor)
@@ -316,6 +368,9 @@ class SudokuNode:
     def _on_NO_SOLUTION(self, msg):
         self._failed(msg.get("uuid"), msg.get("range"), msg.get("sudoku"))
 
+    def _on_EXHAUSTED(self, msg):
+        self._failed(msg.get("uuid"), msg.get("range"), msg.get("sudoku"), exhausted=True)
+
     def _on_STATS_REQ(self, msg):
         with self.lock:
             peers = [n for n in self.network if n != self.me]
@@ -398,6 +453,7 @@ class SudokuNode:
         for t in keep:
             self.tasks.put(t)
         self.neighbor_tasks = [t for t in self.neighbor_tasks if not drop(t)]
+        self.hard = [h for h in self.hard if not drop(h.task)]
 
     def _maybe_delegate(self):
         """A free neighbour gets one queued task (DHT_Node.py:491-498) -- only while this node
@@ -424,27 +480,34 @@ class SudokuNode:
             self._work.notify()
 
     def _worker_loop(self):
+        """New TASKs first (one batched launch per drained queue); between batches, one slice of
+        the oldest budget-hit search (round robin), so a long search never delays new puzzles by
+        more than one bounded launch."""
         while self.running:
             with self._work:
-                while self.running and (self.tasks.empty() or not self._go.is_set()):
+                while self.running and ((self.tasks.empty() and not self.hard) or not self._go.is_set()):
                     self._work.wait(0.5)
             if not self.running:
                 return
             with self.lock:
                 batch = [t for t in self._drain_queue() if t.get("uuid") not in self.done_uuids]
+                hard = None if batch or not self.hard else self.hard.pop(0)
                 self.busy = True
+            work = batch if batch else ([hard.task] if hard else [])
             try:
                 if batch:
                     self._run_batch(batch)
+                elif hard:
+                    self._run_slice(hard)
             except Exception as e:      # the worker must survive a failed launch (ADVICE r1)
-                self._log("batch failed:", repr(e))
-                for t in batch:
-                    self._wake(t.get("uuid"), None, error=repr(e))
+                self._log("launch failed:", repr(e))
+                for t in work:
+                    self._wake(t.get("uuid"), "error", error=repr(e))
             finally:
                 with self.lock:
                     self.busy = False
                     pred = self.predecessor
-                    idle = self.tasks.empty()
+                    idle = self.tasks.empty() and not self.hard
             if idle and pred and pred != self.me:
                 self.send({"method": "NEEDWORK"}, pred)        # DHT_Node.py:245-248
 
@@ -472,37 +535,70 @@ class SudokuNode:
                 return
         self.send(half, nb)
 
-    def _run_batch(self, batch):
-        """All queued TASKs in one sdk_solve_batch launch."""
-        self._split_for_neighbor(batch)
-        boards = np.stack([encode_solve_grid(t["sudoku"]) for t in batch])
-        masks = np.array([range_to_mask(t.get("range", range(1, 10))) for t in batch], dtype=np.uint16)
-        out, status, work = self.engine.solve_batch(boards, masks, want_work=True)
-        nodes = int(work.sum())
+    def _spent(self, nodes):
         if self.delay_ms > 0:
             time.sleep(self.delay_ms * nodes / 1000.0)
         with self.lock:
             self.validations += nodes
-        for t, o, st in zip(batch, out, status):
-            uid = t.get("uuid")
-            if st == L.SDK_SOLVED:
-                grid = [list(row) for row in t["sudoku"]]
-                for r in range(9):
-                    for c in range(9):
-                        if grid[r][c] == 0:
-                            grid[r][c] = int(o[9 * r + c])
-                self._solved(t, grid)
+
+    def _run_batch(self, batch):
+        """All queued TASKs in one bounded launch (node_budget nodes per board)."""
+        self._split_for_neighbor(batch)
+        boards = np.stack([encode_solve_grid(t["sudoku"]) for t in batch])
+        masks = np.array([range_to_mask(t.get("range", range(1, 10))) for t in batch], dtype=np.uint16)
+        out, status, work = self.engine.solve_batch(boards, masks, want_work=True, budget=self.node_budget)
+        self._spent(int(np.asarray(work).sum()))
+        for t, b, m, o, st in zip(batch, boards, masks, out, status):
+            if st == L.SDK_BUDGET_HIT:
+                # not "no solution": the subtree is unexplored.  Continue it alone, between batches
+                s = LexSearch(self.engine, b, int(m), budget=self.node_budget, width=self.search_width,
+                              max_pending=self.search_max_pending, hit=True)
+                with self.lock:
+                    self.hard.append(_HardTask(t, s, time.monotonic() + self.search_limit_s))
+                self._log("budget hit, continuing", t.get("uuid"))
             else:
-                if st == L.SDK_BUDGET_HIT:
-                    self._log("budget exhausted for", uid)
-                # this task's digit range has no completion (or none within the budget): tell
-                # the HTTP origin, which answers once its puzzle's failed ranges cover 1..9
-                origin = _addr(t.get("initial_node"))
-                if origin is None or origin == self.me:
-                    self._failed(uid, t.get("range"), t["sudoku"])
-                else:
-                    self.send({"method": "NO_SOLUTION", "uuid": uid, "range": t.get("range", range(1, 10)),
-                               "sudoku": t["sudoku"], "node": self.me}, origin)
+                self._task_done(t, int(st), o)
+
+    def _run_slice(self, h):
+        """One bounded slice of a budget-hit task's search (search.LexSearch.step)."""
+        with self.lock:
+            if h.task.get("uuid") in self.done_uuids:
+                return
+        before = h.search.nodes
+        done = h.search.step()
+        self._spent(h.search.nodes - before)
+        if not done and time.monotonic() >= h.deadline:
+            done = True
+            h.search.status = L.SDK_BUDGET_HIT
+        if done:
+            self._task_done(h.task, int(h.search.status), h.search.board)
+        else:
+            with self.lock:
+                self.hard.append(h)
+
+    def _task_done(self, t, st, o):
+        """Report a finished task: its completion, 'no completion in this range' (NO_SOLUTION) or
+        'search exhausted' (EXHAUSTED; the range stays undecided, so no higher-range completion
+        is ever taken for the lex-first one)."""
+        uid = t.get("uuid")
+        if st == L.SDK_SOLVED:
+            grid = [list(row) for row in t["sudoku"]]
+            for r in range(9):
+                for c in range(9):
+                    if grid[r][c] == 0:
+                        grid[r][c] = int(o[9 * r + c])
+            self._solved(t, grid)
+            return
+        exhausted = st == L.SDK_BUDGET_HIT
+        if exhausted:
+            self._log("search exhausted for", uid)
+        # tell the HTTP origin, which answers once its puzzle's ranges are decided
+        origin = _addr(t.get("initial_node"))
+        if origin is None or origin == self.me:
+            self._failed(uid, t.get("range"), t["sudoku"], exhausted=exhausted)
+        else:
+            self.send({"method": "EXHAUSTED" if exhausted else "NO_SOLUTION", "uuid": uid,
+                       "range": t.get("range", range(1, 10)), "sudoku": t["sudoku"], "node": self.me}, origin)
 
     def _solved(self, task, grid):
         """This node completed `task`: SOLUTION_FOUND to every peer (and the HTTP origin).  A
@@ -543,34 +639,49 @@ class SudokuNode:
                 self.done_uuids.add(uid)
                 self._purge(uid)
                 self.best.pop(uid, None)
-                final = grid
+                final = ("solution", grid)
             else:
-                best = self.best.get(uid)
-                if best is None or lo < best[0]:
-                    self.best[uid] = (lo, grid)
+                if uid in self.waiters:              # only the HTTP origin orders completions
+                    best = self.best.get(uid)
+                    if best is None or lo < best[0]:
+                        self.best[uid] = (lo, grid)
                 self._purge(uid, above=lo)
-                final = self._accept(uid)
+                final = self._decide(uid)
         if final is not None:
-            self._wake(uid, final)
+            self._wake(uid, *final)
 
-    def _accept(self, uid):
-        """(under self.lock) The origin's best completion if every digit below its range failed."""
+    def _decide(self, uid):
+        """(under self.lock) The origin's answer once it is determined, else None:
+          ("solution", grid)  the best completion, every digit below its range failed;
+          ("none", None)      every digit of the first empty cell failed;
+          ("exhausted", None) the lowest undecided digit lies in an exhausted range, so no
+                              completion that could still arrive is provably the lex-first one."""
         w = self.waiters.get(uid)
+        if w is None:
+            return None
+        failed, exhausted = w[3]
         best = self.best.get(uid)
-        if w is None or best is None:
-            return None
-        need = ((1 << best[0]) - 1) & ALL_DIGITS_MASK          # digits 1 .. lo-1
-        if (w[3][0] & need) != need:
-            return None
-        self.done_uuids.add(uid)
-        self._purge(uid)
-        del self.best[uid]
-        return best[1]
+        verdict = None
+        if best is not None:
+            need = ((1 << best[0]) - 1) & ALL_DIGITS_MASK      # digits 1 .. lo-1
+            if (failed & need) == need:
+                verdict = ("solution", best[1])
+        if verdict is None:
+            rest = ALL_DIGITS_MASK & ~failed
+            if rest == 0:
+                verdict = ("none", None)
+            elif exhausted & rest & -rest:
+                verdict = ("exhausted", None)
+        if verdict is not None:
+            self.done_uuids.add(uid)
+            self._purge(uid)
+            self.best.pop(uid, None)
+        return verdict
 
-    def _failed(self, uid, arr, sudoku):
-        """A range of puzzle `uid` has no completion: the HTTP origin answers once the failed
-        ranges cover every digit of the first empty cell (only reports about its own board
-        count), or accepts a waiting upper-range completion once everything below it failed."""
+    def _failed(self, uid, arr, sudoku, exhausted=False):
+        """A range of puzzle `uid` has no completion (or, `exhausted`, its search gave up): the
+        HTTP origin answers once the ranges are decided (_decide; only reports about its own
+        board count)."""
         try:
             m = range_to_mask(arr if arr is not None else range(1, 10))
             board = encode_solve_grid(sudoku)
@@ -580,21 +691,17 @@ class SudokuNode:
             w = self.waiters.get(uid)
             if w is None or not np.array_equal(w[2], board):
                 return
-            w[3][0] |= m
-            final = self._accept(uid)
-            none_left = final is None and (w[3][0] & ALL_DIGITS_MASK) == ALL_DIGITS_MASK
-            if none_left:
-                self.done_uuids.add(uid)
+            w[3][1 if exhausted else 0] |= m
+            final = self._decide(uid)
         if final is not None:
-            self._wake(uid, final)
-        elif none_left:
-            self._wake(uid, None)
+            self._wake(uid, *final)
 
-    def _wake(self, uid, solution, error=None):
+    def _wake(self, uid, kind, solution=None, error=None):
         with self.lock:
             w = self.waiters.get(uid)
         if w is not None:
-            w[1].append(solution if error is None else _Failure(error))
+            w[1].append(_Failure(error) if error is not None else
+                        (_EXHAUSTED if kind == "exhausted" else solution))
             w[0].set()
 
     # ------------------------------------------------------------- HTTP side
@@ -605,7 +712,7 @@ class SudokuNode:
         task = {"method": "TASK", "sudoku": puzzle, "range": range(1, 10), "uuid": uid, "initial_node": self.me}
         _validate_task(task)
         with self.lock:
-            self.waiters[uid] = (ev, box, encode_solve_grid(puzzle), [0])
+            self.waiters[uid] = (ev, box, encode_solve_grid(puzzle), [0, 0])
         self.enqueue(task)
         ok = ev.wait(self.solve_timeout_s)
         with self.lock:
@@ -616,6 +723,9 @@ class SudokuNode:
         res = box[0] if box else None
         if isinstance(res, _Failure):
             raise RuntimeError(f"solve failed: {res.error}")
+        if res is _EXHAUSTED:
+            raise SearchExhaustedError("search exhausted: no answer within the node's search limits "
+                                       "(the reference would still be searching, DHT_Node.py:553-554)")
         return res
 
     def stats(self):
@@ -672,6 +782,13 @@ class _Failure:
         self.error = error
 
 
+_EXHAUSTED = object()
+
+
+class SearchExhaustedError(Exception):
+    """POST /solve of a puzzle whose search gave up (HTTP 504, "exhausted": true)."""
+
+
 def _validate_task(msg):
     """Raise unless a TASK can be launched: a 9x9 (or flat 81) grid and an ascending 0..9 range."""
     encode_solve_grid(msg["sudoku"])
@@ -710,6 +827,9 @@ class _Handler(BaseHTTPRequestHandler):
             return self._reply(400, {"error": str(e)})
         try:
             solution = node.solve_http(puzzle)
+        except SearchExhaustedError as e:
+            return self._reply(504, {"error": str(e), "solution": None, "exhausted": True,
+                                     "duration": time.time() - t0})
         except TimeoutError as e:
             return self._reply(504, {"error": str(e)})
         except (ValueError, TypeError) as e:

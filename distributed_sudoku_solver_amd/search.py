@@ -1,0 +1,183 @@
+"""Resumable, budgeted lex-first search of one board (SURVEY §7 hard parts 2 and 7).
+
+The reference's solve_sudoku (DHT_Node.py:474-538) searches until its DFS ends -- on
+a board that propagation cannot refute (e.g. '55' + 79 zeros) that is
+never, and its POST /solve waits forever (DHT_Node.py:553-554).  A GPU launch that
+never ends is worse still: it holds every other board of its batch.  So every
+product-path solve here is bounded:
+
+  * a launch gives each board a node budget (sdk_solve_batch_budget); a board that
+    runs out comes back as SDK_BUDGET_HIT -- a state of its own, never "no solution" --
+    and its launch ends with the rest of the batch answered;
+  * such a board is continued by LexSearch, in slices of bounded time: an ordered
+    worklist of sub-boards whose completions, taken in worklist order, are exactly the
+    board's completions in lex order.  Each slice solves the first `width` sub-boards in
+    ONE launch (each with the budget) and replaces every sub-board that hit the budget by
+    its children (sdk_expand_boards: the reference's branching -- lowest open cell,
+    digits ascending -- after propagation, one batched call on the GPU).  The first
+    SOLVED sub-board whose predecessors are all refuted holds the reference's answer
+    (its lex-first completion); later sub-boards are dropped as soon as one solves.
+  * the worklist only ever goes deeper, so the search ends on every board the engine
+    can finish; a board whose worklist outgrows `max_pending` sub-boards, or whose caller's
+    deadline passes, ends as SDK_BUDGET_HIT ("search exhausted"): a defined answer that
+    is never confused with "no completion" (node.py keeps digit ranges lex-ordered on it).
+
+A slice is one launch plus at most one expansion call, so a node's worker can
+interleave new requests with a long search between slices (node.py).  The search
+runs on whatever engine it is given: SudokuEngine (libsudoku_hip.so) in the product,
+an oracle double in the CPU tests.
+"""
+import collections
+import time
+
+import numpy as np
+
+from . import _lib as L
+from .engine import ALL_DIGITS_MASK
+
+DEFAULT_BUDGET = 2048          # search nodes per board per launch (a ~10 ms bound on MI355X)
+DEFAULT_WIDTH = 16384          # sub-boards per slice (fills the solver's resident slots)
+DEFAULT_MAX_PENDING = 1 << 20  # sub-boards the worklist may hold (81 MB of host memory)
+
+
+class LexSearch:
+    """The reference's answer for one board, found in bounded slices.
+
+    engine   anything with solve_batch(boards, masks, want_work, budget) and
+             expand(boards, masks, target) -- SudokuEngine on the GPU
+    board    uint8[81] (0 empty, 1..9 given, 10..255 inert given)
+    mask     first-cell digit mask (the TASK `range`, engine.range_to_mask), None = all
+    hit      the board already hit the budget in a batch launch: start by expanding it
+
+    After step() returned True, `status` is SDK_SOLVED (board = the lex-first completion),
+    SDK_UNSOLVABLE (board = the input: the reference restores it) or SDK_BUDGET_HIT
+    (exhausted: the worklist outgrew max_pending, or run()'s deadline passed)."""
+
+    def __init__(self, engine, board, mask=None, budget=DEFAULT_BUDGET, width=DEFAULT_WIDTH,
+                 max_pending=DEFAULT_MAX_PENDING, hit=False):
+        if budget < 1 or width < 1:
+            raise ValueError("budget and width must be >= 1")
+        self.engine = engine
+        self.input = np.ascontiguousarray(board, dtype=np.uint8).reshape(81).copy()
+        self.budget = int(budget)
+        self.width = int(width)
+        self.max_pending = int(max_pending)
+        root_mask = ALL_DIGITS_MASK if mask is None else int(mask)
+        # worklist: chunks (boards uint8[k,81], masks uint16[k]) in lex order of their subtrees
+        self._chunks = collections.deque([(self.input[None].copy(), np.array([root_mask], np.uint16))])
+        self._pending = 1
+        self._expand_first = bool(hit)
+        self.best = None          # lex-first completion found so far (only unrefuted boards precede it)
+        self.status = None
+        self.nodes = 0            # engine work (search nodes) spent
+        self.launches = 0
+        self.expansions = 0
+        self.slices = 0
+
+    # ----------------------------------------------------------------- worklist
+    def _take(self, k):
+        boards, masks, got = [], [], 0
+        while self._chunks and got < k:
+            b, m = self._chunks.popleft()
+            if got + len(b) > k:
+                cut = k - got
+                self._chunks.appendleft((b[cut:], m[cut:]))
+                b, m = b[:cut], m[:cut]
+            boards.append(b)
+            masks.append(m)
+            got += len(b)
+        self._pending -= got
+        if len(boards) == 1:
+            return boards[0], masks[0]
+        return np.concatenate(boards), np.concatenate(masks)
+
+    def _push_front(self, boards, masks):
+        if len(boards):
+            self._chunks.appendleft((boards, masks))
+            self._pending += len(boards)
+
+    def _expand(self, boards, masks):
+        kids = self.engine.expand(boards, masks, target=max(self.width, 2 * len(boards)))
+        self.expansions += 1
+        return kids, np.full(len(kids), ALL_DIGITS_MASK, np.uint16)   # a mask lives in level 0 only
+
+    @property
+    def pending(self):
+        return self._pending
+
+    @property
+    def done(self):
+        return self.status is not None
+
+    @property
+    def board(self):
+        return self.best.copy() if self.status == L.SDK_SOLVED else self.input.copy()
+
+    def _finish(self, status):
+        self.status = status
+        self._chunks.clear()
+        self._pending = 0
+
+    # -------------------------------------------------------------------- slice
+    def step(self):
+        """One slice: one launch over the worklist's front (+ one expansion call).  Returns done."""
+        if self.status is not None:
+            return True
+        self.slices += 1
+        if self._expand_first:
+            self._expand_first = False
+            b, m = self._take(self._pending)
+            self._push_front(*self._expand(b, m))
+        if self._pending == 0:
+            self._finish(L.SDK_SOLVED if self.best is not None else L.SDK_UNSOLVABLE)
+            return True
+        boards, masks = self._take(self.width)
+        out, st, work = self.engine.solve_batch(boards, masks, want_work=True, budget=self.budget)
+        self.launches += 1
+        if work is not None:
+            self.nodes += int(np.asarray(work, dtype=np.uint64).sum())
+        st = np.asarray(st)
+        decided = np.flatnonzero(st != L.SDK_UNSOLVABLE)          # refuted sub-boards simply vanish
+        solved = decided[st[decided] == L.SDK_SOLVED]
+        first = int(solved[0]) if len(solved) else None
+        hits = decided if first is None else decided[decided < first]
+        if first is not None:
+            # every sub-board after it (the rest of the slice and the worklist) is lex-greater
+            self.best = np.array(out[first], dtype=np.uint8)
+            self._chunks.clear()
+            self._pending = 0
+        if len(hits):
+            self._push_front(*self._expand(boards[hits], masks[hits]))
+        if self._pending == 0:
+            self._finish(L.SDK_SOLVED if self.best is not None else L.SDK_UNSOLVABLE)
+            return True
+        if self._pending > self.max_pending:
+            self._finish(L.SDK_BUDGET_HIT)
+            return True
+        return False
+
+    def run(self, deadline=None):
+        """Slices until done or time.monotonic() passes `deadline` (then SDK_BUDGET_HIT)."""
+        while not self.step():
+            if deadline is not None and time.monotonic() >= deadline:
+                self._finish(L.SDK_BUDGET_HIT)
+                break
+        return self.status, self.board
+
+
+def solve_bounded(engine, boards, masks=None, budget=DEFAULT_BUDGET, time_limit=None, width=DEFAULT_WIDTH,
+                  max_pending=DEFAULT_MAX_PENDING):
+    """solve_batch with every board bounded: one launch at `budget` nodes per board, then a
+    LexSearch per board that hit it, each until done or `time_limit` seconds (None = no limit).
+    Returns (out, status, work) like solve_batch; status SDK_BUDGET_HIT = search exhausted."""
+    boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
+    out, st, work = engine.solve_batch(boards, masks, want_work=True, budget=budget)
+    out, st = np.array(out), np.array(st)
+    work = np.zeros(len(boards), np.uint64) if work is None else np.array(work, dtype=np.uint64)
+    for i in np.flatnonzero(st == L.SDK_BUDGET_HIT):
+        m = None if masks is None else int(np.asarray(masks)[i])
+        s = LexSearch(engine, boards[i], m, budget=budget, width=width, max_pending=max_pending, hit=True)
+        s.run(None if time_limit is None else time.monotonic() + time_limit)
+        out[i], st[i] = s.board, s.status
+        work[i] += np.uint64(s.nodes)
+    return out, st, work

@@ -73,7 +73,19 @@ class ShardedBatch:
         self.rank = rank
         self.world = world
         self.root = root
+        self._own_comm = comm is None and group is None and world > 1   # made here: closed by close()
         self.comm = _host_transport(rank, world, comm, group)
+
+    def close(self):
+        if self._own_comm and self.comm is not None:
+            self.comm.close()
+        self.comm = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def _gather(self, local):
         if self.world == 1:
@@ -219,7 +231,13 @@ class RcclComm:
         if _attach:
             return
         if uid is None:
-            uid = self.exchange_id(rank, _host_transport(rank, world, transport, group) if world > 1 else None)
+            own = world > 1 and transport is None and group is None
+            t = _host_transport(rank, world, transport, group) if world > 1 else None
+            try:
+                uid = self.exchange_id(rank, t)
+            finally:
+                if own and t is not None:
+                    t.close()                    # the implicit transport carried the id only
         engine.comm_init(uid, rank, world)
 
     @classmethod
@@ -227,10 +245,9 @@ class RcclComm:
         """Wrap an engine whose context already has a communicator (open_clique)."""
         return cls(engine, rank, world, _attach=True)
 
-    @staticmethod
-    def exchange_id(rank, transport):
-        from .engine import SudokuEngine
-        uid = SudokuEngine.comm_unique_id() if rank == 0 else None
+    def exchange_id(self, rank, transport):
+        """Rank 0's RCCL id (engine.comm_unique_id) on every rank, over the host transport."""
+        uid = self.engine.comm_unique_id() if rank == 0 else None
         if transport is None:
             return uid
         return transport.broadcast_bytes(uid, 0)

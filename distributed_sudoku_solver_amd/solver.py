@@ -18,14 +18,29 @@ search nodes for the propagating solvers (the naive-DFS count is not defined for
 propagating search), or exactly the reference's validations when the
 engine runs the one-board-per-lane reference DFS (SDK_OPT_SOLVER = SDK_SOLVER_LANE;
 slow on hard boards, exact /stats accounting).
+
+Every solve is bounded (search.LexSearch): launches of DEFAULT_BUDGET nodes per board,
+a board that needs more is continued in slices over its lex-ordered frontier until it
+is decided or `time_limit` passes.  Then solve_grid raises SearchExhausted, and the
+mixins return False WITHOUT any side effect -- exactly what a reference node whose
+solve_sudoku is still running shows its peers (perform_solving sends nothing on
+False, DHT_Node.py:424-470), but its node thread is free again.
 """
 import threading
+import time
 
 import numpy as np
 
 from .engine import SudokuEngine, encode_solve_grid, range_to_mask
+from .search import DEFAULT_BUDGET, LexSearch
 from .utils import split_array_in_middle
 from . import _lib as L
+
+DEFAULT_TIME_LIMIT_S = 60.0
+
+
+class SearchExhausted(L.SudokuHipError):
+    """The bounded search gave up (time limit or worklist size): the board is undecided."""
 
 _engines = {}
 _engines_lock = threading.Lock()
@@ -35,7 +50,8 @@ def default_engine(device=0):
     with _engines_lock:
         eng = _engines.get(device)
         if eng is None:
-            eng = _engines[device] = SudokuEngine(device)
+            # bounded by default: a direct solve_batch on it never runs unbounded either
+            eng = _engines[device] = SudokuEngine(device, node_budget=DEFAULT_BUDGET)
         return eng
 
 
@@ -43,21 +59,33 @@ def _empty_cells(puzzle):
     return [(r, c) for r in range(9) for c in range(9) if puzzle[r][c] == 0]
 
 
-def solve_grid(puzzle, arr=range(1, 10), engine=None):
-    """Core drop-in: mutate `puzzle` like the reference solver and return (ok, work)."""
+def solve_grid(puzzle, arr=range(1, 10), engine=None, budget=DEFAULT_BUDGET, time_limit=DEFAULT_TIME_LIMIT_S):
+    """Core drop-in: mutate `puzzle` like the reference solver and return (ok, work).
+
+    Bounded (module docstring): raises SearchExhausted when the search gives up."""
     eng = engine or default_engine()
     board = encode_solve_grid(puzzle)
-    mask = np.array([range_to_mask(arr)], dtype=np.uint16)
-    out, status, work = eng.solve_batch(board[None, :], mask, want_work=True)
-    st = int(status[0])
+    search = LexSearch(eng, board, range_to_mask(arr), budget=budget)
+    st, sol = search.run(None if time_limit is None else time.monotonic() + time_limit)
     if st == L.SDK_BUDGET_HIT:
-        raise L.SudokuHipError("node budget exhausted (SDK_OPT_NODE_BUDGET); the reference would still be searching")
+        raise SearchExhausted(f"search exhausted after {search.nodes} nodes in {search.launches} launches; "
+                              "the reference would still be searching (DHT_Node.py:474-538)")
     if st == L.SDK_SOLVED:
-        sol = out[0]
         for r, c in _empty_cells(puzzle):
             puzzle[r][c] = int(sol[9 * r + c])
-        return True, int(work[0])
-    return False, int(work[0])
+        return True, search.nodes
+    return False, search.nodes
+
+
+def _solve_or_idle(node, puzzle, arr):
+    """solve_grid for the mixins: an exhausted search is reported as False with no side
+    effect (the reference node would still be searching and would have sent nothing)."""
+    try:
+        ok, work = solve_grid(puzzle, arr, node.sudoku_engine)
+    except SearchExhausted:
+        return False
+    node.validations += work
+    return ok
 
 
 def solve_sudoku(puzzle, arr=range(1, 10), engine=None):
@@ -92,9 +120,7 @@ class HipSolveMixin:
                 self.send_data(task, self.neighbor)
                 self.neighbor_tasks.put(task)
                 self.neighborfree = False
-        ok, work = solve_grid(puzzle, arr, self.sudoku_engine)
-        self.validations += work
-        return ok
+        return _solve_or_idle(self, puzzle, arr)
 
 
 class HipSolveMixinMain:
@@ -114,6 +140,4 @@ class HipSolveMixinMain:
             first_half, arr = split_array_in_middle(arr)
             self.send_data({"method": "TASK", "sudoku": puzzle, "range": first_half}, self.neighbor)
             self.neighborfree = False
-        ok, work = solve_grid(puzzle, arr, self.sudoku_engine)
-        self.validations += work
-        return ok
+        return _solve_or_idle(self, puzzle, arr)

@@ -139,6 +139,31 @@ int sdk_check_batch_i64(sdk_ctx *ctx, const int64_t *boards, uint8_t *verdict, s
 int sdk_solve_batch(sdk_ctx *ctx, const uint8_t *in, const uint16_t *first_cell_mask,
                     uint8_t *out, int8_t *status, uint64_t *work, size_t n);
 
+/* sdk_solve_batch with the node budget of THIS call (search nodes per board, 0 =
+ * unlimited, SDK_BUDGET_CONTEXT = the context's SDK_OPT_NODE_BUDGET): callers that
+ * share a context (several ring nodes on one GPU) bound their own launches without
+ * touching the shared option.  A board that runs out is SDK_BUDGET_HIT -- never
+ * SDK_UNSOLVABLE: its subtree is unexplored, not empty (the reference would still be
+ * searching, DHT_Node.py:474-538).  Its launch ends anyway, so one hard board cannot
+ * hold back the rest of its batch. */
+#define SDK_BUDGET_CONTEXT UINT64_MAX
+int sdk_solve_batch_budget(sdk_ctx *ctx, const uint8_t *in, const uint16_t *first_cell_mask,
+                           uint8_t *out, int8_t *status, uint64_t *work, size_t n, uint64_t node_budget);
+
+/* The worklist step of a resumable lex-first search of a board whose solve hit the
+ * budget (distributed_sudoku_solver_amd/search.py; the in-node form of handing a
+ * subtree on, DHT_Node.py:491-510): expand n boards -- board i with first-cell mask
+ * first_cell_masks[i] (nullable = range(1,10) everywhere) -- breadth-first in the
+ * reference's DFS order (lowest open cell after propagation, digits ascending, solved
+ * boards kept, contradicted ones dropped), at least one level deep and on until the
+ * frontier holds >= target boards or nothing branches.  The frontier goes to `out`
+ * (*out_n boards, uint8[*out_n][81]); children keep their parents' order, so board k's
+ * completions all precede board k+1's in lex order, and the union of their completions
+ * is exactly the seeds'.  cap = capacity of `out` in boards; cap >= 9 * max(n, target)
+ * always suffices (SDK_EINVAL if the frontier does not fit). */
+int sdk_expand_boards(sdk_ctx *ctx, const uint8_t *boards, const uint16_t *first_cell_masks, size_t n,
+                      uint64_t target, uint8_t *out, size_t cap, uint64_t *out_n);
+
 /* Counts completions of one board (same constraint as the solver), stopping
  * at `limit` (0 = no limit).  status as above. */
 int sdk_count_solutions(sdk_ctx *ctx, const uint8_t *board, uint64_t limit,

@@ -3,6 +3,57 @@ import numpy as np
 
 from distributed_sudoku_solver_amd import _lib as L
 
+# the doubles' naive DFS needs far more validations than the GPU engine needs search nodes:
+# a node budget b allows b * this many validations
+VALIDATIONS_PER_NODE = 10_000
+
+
+def validation_budget(budget, default):
+    """Node budget of a solve_batch call -> the oracle's validation budget."""
+    return default if budget is None else (0 if budget == 0 else int(budget) * VALIDATIONS_PER_NODE)
+
+
+def naive_children(b):
+    """Children of a board in the reference's DFS order (lowest empty cell, valid digits
+    ascending, utils.py:14-56) -- None if the board is complete."""
+    z = np.flatnonzero(b == 0)
+    if len(z) == 0:
+        return None
+    c = int(z[0])
+    r, col = divmod(c, 9)
+    br, bc = 3 * (r // 3), 3 * (col // 3)
+    used = set(b[9 * r: 9 * r + 9].tolist()) | set(b[col::9].tolist()) | {
+        int(b[9 * (br + i) + bc + j]) for i in range(3) for j in range(3)}
+    out = []
+    for d in range(1, 10):
+        if d not in used:
+            ch = b.copy()
+            ch[c] = d
+            out.append((ch, d))
+    return out
+
+
+def naive_expand(boards, masks=None, target=64):
+    """CPU restatement of sdk_expand_boards without propagation: level 0 always (board i's
+    first empty cell restricted to masks[i]), then on while < target boards and something
+    branches.  Complete boards stay; boards with no valid digit vanish."""
+    fr = [np.asarray(b, dtype=np.uint8).copy() for b in np.asarray(boards).reshape(-1, 81)]
+    allowed = [None] * len(fr) if masks is None else [int(m) for m in np.asarray(masks).reshape(-1)]
+    level = 0
+    while fr and (level == 0 or len(fr) < target):
+        nxt, grew = [], False
+        for b, m in zip(fr, allowed):
+            kids = naive_children(b)
+            if kids is None:
+                nxt.append(b)
+                continue
+            grew = True
+            nxt += [ch for ch, d in kids if m is None or (m >> d) & 1]
+        fr, allowed, level = nxt, [None] * len(nxt), level + 1
+        if not grew:
+            break
+    return np.stack(fr) if fr else np.zeros((0, 81), np.uint8)
+
 
 class OracleEngine:
     """Test double with the SudokuEngine batch interface, computed by the oracle."""
@@ -12,10 +63,15 @@ class OracleEngine:
         self.O = O
         self.calls = []
 
-    def solve_batch(self, boards, masks=None, want_work=False):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
         self.calls.append(len(boards))
-        out, st, val = self.O.naive_solve_batch(boards, masks, budget=50_000_000, threads=2)
+        out, st, val = self.O.naive_solve_batch(boards, masks, budget=validation_budget(budget, 50_000_000),
+                                                threads=2)
         return out, st, (val if want_work else None)
+
+    def expand(self, boards, masks=None, target=64):
+        self.calls.append(("expand", len(boards)))
+        return naive_expand(boards, masks, target)
 
     def check_batch(self, boards):
         self.calls.append(len(boards))
@@ -110,22 +166,56 @@ class _HostBuffer:
         self.data = None
 
 
-class BenchStubEngine:
+class BenchStubEngine(OracleEngine):
     """The device-buffer interface bench.py drives, computed by the oracle on the host:
-    lets the CPU tests run bench.py's rank launcher and sharding logic (no GPU here)."""
+    lets the CPU tests run bench.py's rank launcher and sharding logic (no GPU here).
+    Its "RCCL" is a TcpComm of its own, set up from the id the ranks exchange (an RCCL stub):
+    the C5 legs run their real collective pattern through the bench's own transports."""
+
+    _DT = {L.SDK_COMM_U64: np.uint64, L.SDK_COMM_I64: np.int64, L.SDK_COMM_U8: np.uint8}
+    _OP = {L.SDK_COMM_SUM: "sum", L.SDK_COMM_MIN: "min", L.SDK_COMM_MAX: "max"}
 
     def __init__(self, device=0):
-        from oracle import oracle as O
-        self.O = O
+        super().__init__()
         self.device = device
         self.opts = {}
         self.launches = 0
+        self._comm = None
 
     def set_option(self, key, value):
         self.opts[key] = int(value)
 
     def get_option(self, key):
+        if key in (L.SDK_OPT_DEVICE_CUS, L.SDK_OPT_WAVES_PER_CU) and key not in self.opts:
+            return super().get_option(key)
         return self.opts.get(key, 0)
+
+    # ---- RCCL stub: id = a free TCP port for a second TcpComm between the ranks ----
+    @staticmethod
+    def comm_unique_id():
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        return port.to_bytes(4, "little") + bytes(L.SDK_COMM_ID_BYTES - 4)
+
+    def comm_init(self, uid, rank, world):
+        from distributed_sudoku_solver_amd.hostcomm import TcpComm
+        self._comm = TcpComm(rank, world, port=int.from_bytes(uid[:4], "little"))
+
+    def comm_destroy(self):
+        if self._comm is not None:
+            self._comm.close()
+        self._comm = None
+
+    def comm_allreduce(self, buf, count, dtype, op):
+        self._comm.allreduce(buf, count, self._DT[dtype], self._OP[op])
+
+    def comm_broadcast(self, buf, nbytes, root):
+        self._comm.broadcast(buf, nbytes, root)
+
+    def comm_allgather(self, send, recv, nbytes):
+        self._comm.allgather(send, recv, nbytes)
 
     def alloc(self, nbytes):
         return _HostBuffer(nbytes)

@@ -1,7 +1,9 @@
 """bench.py's rank launcher and C4 sharding on the CPU: `--gpus 2` without torchrun starts two
-rank processes (gloo barrier / max), each solves its contiguous slice of the SAME seeded stream
+rank processes (TcpComm barrier / max), each solves its contiguous slice of the SAME seeded stream
 (strong scaling), and rank 0 prints one JSON line with n_gpus == 2.  The oracle stands in for the
-GPU (tests/doubles.BenchStubEngine)."""
+GPU (tests/doubles.BenchStubEngine, whose RCCL stub is a TcpComm set up from the exchanged id).
+Every run blocks `import torch` in every process (a sitecustomize on PYTHONPATH): the bench and
+its multi-rank path are torch-free."""
 import json
 import os
 import subprocess
@@ -10,8 +12,28 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run_bench(gpus, extra=()):
-    env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "tests")]))
+NO_TORCH = """
+import sys
+
+
+class _NoTorch:
+    def find_spec(self, name, path=None, target=None):
+        if name == "torch" or name.startswith("torch."):
+            raise ImportError("bench.py must not import torch (VERDICT r2 item 5)")
+        return None
+
+
+sys.meta_path.insert(0, _NoTorch())
+"""
+
+
+def _run_bench(gpus, extra=(), tmp=None):
+    paths = [ROOT, os.path.join(ROOT, "tests")]
+    if tmp is not None:
+        with open(os.path.join(tmp, "sitecustomize.py"), "w") as f:
+            f.write(NO_TORCH)
+        paths.insert(0, str(tmp))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join(paths))
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "2", "--warmup", "1",
            "--workload", "solve30", "--batch", "301", "--check-boards", "2000", "--check-steps", "1",
@@ -25,8 +47,8 @@ def _run_bench(gpus, extra=()):
     return json.loads(lines[0])
 
 
-def test_bench_gpus2_launches_two_ranks():
-    r = _run_bench(2)
+def test_bench_gpus2_launches_two_ranks(tmp_path):
+    r = _run_bench(2, tmp=tmp_path)
     assert r["n_gpus"] == 2 and r["scaling"] == "strong"
     assert r["config"]["puzzles_total"] == 301 and r["config"]["puzzles_per_gpu"] in (150, 151)
     assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 301}
@@ -35,7 +57,27 @@ def test_bench_gpus2_launches_two_ranks():
     assert r["value"] > 0 and r["steps"] == 2 and r["warmup"] == 1
 
 
-def test_bench_gpus1_single_process():
-    r = _run_bench(1)
+def test_bench_gpus1_single_process(tmp_path):
+    r = _run_bench(1, tmp=tmp_path)
     assert r["n_gpus"] == 1 and "weak_scaling" not in r
     assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 301}
+
+
+def test_bench_gpus2_count_legs_over_tcp_rccl_stub(tmp_path):
+    """the C5 legs at world 2 -- RCCL id over the ranks' TcpComm, the two-stage
+    count's all-reduce and the rebalanced count's all-gathers through the stub -- with torch blocked."""
+    r = _run_bench(2, extra=["--count-leg", "1", "--c5-boards", "16,16", "--frontier-probe", "0"], tmp=tmp_path)
+    for leg in ("c5_count", "c5_count_rebalanced"):
+        assert r[leg].get("ok") is True, r[leg]
+        assert r[leg]["solutions"] == 7309
+    assert r["c5_count_rebalanced"]["rounds"] >= 1
+
+
+def test_no_torch_blocker_works(tmp_path):
+    """The blocker the bench tests rely on does stop a torch import."""
+    import subprocess
+    with open(os.path.join(tmp_path, "sitecustomize.py"), "w") as f:
+        f.write(NO_TORCH)
+    env = dict(os.environ, PYTHONPATH=str(tmp_path))
+    p = subprocess.run([sys.executable, "-c", "import torch"], env=env, capture_output=True, text=True)
+    assert p.returncode != 0 and "must not import torch" in p.stderr

@@ -52,9 +52,12 @@ class _Counting:
     def __init__(self, eng):
         self.eng, self.sizes = eng, []
 
-    def solve_batch(self, boards, masks=None, want_work=False):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
         self.sizes.append(len(boards))
-        return self.eng.solve_batch(boards, masks, want_work)
+        return self.eng.solve_batch(boards, masks, want_work, budget)
+
+    def expand(self, boards, masks=None, target=64):
+        return self.eng.expand(boards, masks, target)
 
 
 def test_concurrent_posts_batch_into_few_launches(engine):
@@ -128,3 +131,56 @@ def test_main_api_and_main_mixin_on_gpu(engine, solve_cases):
         grid = [list(c["puzzle"][9 * r: 9 * r + 9]) for r in range(9)]
         assert nd.solve_sudoku(grid, range(*c["range"])) == c["ok"], c["name"]
         assert [v for row in grid for v in row] == (c["board"] if c["ok"] else c["puzzle"]), c["name"]
+
+
+# ------------------------------------------------------------- bounded solves (SURVEY §7 hard parts 2, 7)
+def test_conflict55_beside_wiki_on_gpu_node(engine):
+    """'55'+79 zeros and the wiki puzzle POSTed concurrently.  The wiki answer is
+    201 and exact within 50 ms, /stats keeps answering, the conflict board gets the documented 504
+    {"solution": null, "exhausted": true}."""
+    import threading
+    from test_node import CONFLICT55, _post_any
+    node = SudokuNode("127.0.0.1", 0, 0, engine=engine, delay_ms=0, search_limit_s=10.0).start()
+    try:
+        _post(node.http_port, _grid(synth.WIKI))                      # warm
+        res = {}
+        th = threading.Thread(target=lambda: res.__setitem__("c", _post_any(node.http_port, _grid(CONFLICT55))))
+        th.start()
+        wiki = []
+        for _ in range(5):
+            code, body = _post(node.http_port, _grid(synth.WIKI))
+            assert code == 201 and "".join(str(v) for row in body["solution"] for v in row) == synth.WIKI_SOLUTION
+            wiki.append(body["duration"])
+            code, st = _get(node.http_port, "/stats")
+            assert code == 200
+        th.join(60)
+        code, body = res["c"]
+        assert code == 504 and body["exhausted"] is True and body["solution"] is None, (code, body)
+        assert max(wiki) < 0.05, wiki
+        code, body = _post(node.http_port, _grid(synth.WIKI))
+        assert code == 201 and body["duration"] < 0.05
+    finally:
+        _stop([node])
+
+
+def test_split_with_budget_hit_lower_half_on_gpu(engine):
+    """The HIP origin keeps range(1, 5) of DEMO8 and every launch it makes hits the budget (1 node);
+    the oracle neighbour answers range(5, 10) first; the origin still returns the golden lex-first
+    board, and never reports its budget-hit range as failed."""
+    from test_node import DEMO8, DEMO8_FIRST, OracleEngine
+    a = SudokuNode("127.0.0.1", 0, 0, engine=engine, delay_ms=0, trace=True, node_budget=1).start()
+    b = SudokuNode("127.0.0.1", 0, 0, anchor=a.me, engine=OracleEngine(), delay_ms=0, trace=True).start()
+    try:
+        assert b.wait_joined()
+        t0 = time.time()
+        while not a.neighborfree and time.time() - t0 < 5:
+            time.sleep(0.01)
+        code, body = _post(a.http_port, _grid(DEMO8))
+        assert code == 201 and "".join(str(v) for row in body["solution"] for v in row) == DEMO8_FIRST
+        assert [t for t in a.trace if t[0] == "TASK"][0][1:] == (b.me, range(5, 10))
+        assert not any(t[0] == "NO_SOLUTION" for t in a.trace)
+        for name in ("S1", "S3"):
+            code, body = _post(a.http_port, _grid(synth.SEEDS17[name]))
+            assert "".join(str(v) for row in body["solution"] for v in row) == synth.SEED_SOLUTIONS[name]
+    finally:
+        _stop([a, b])

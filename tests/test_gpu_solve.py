@@ -511,3 +511,41 @@ def test_host_pointer_large_batch(engine):
     masks = np.full(n, O.range_mask(1, 10), dtype=np.uint16)
     out, st, work = engine.solve_batch(p, masks, want_work=True)
     assert (st == 1).all() and (out == s).all() and (work >= 1).all()
+
+
+def _count_all(engine, size):
+    res = engine.result_buffer(2, np.uint64)
+    try:
+        engine.frontier_count(0, 1, size, 0, res)
+        cnt, hits = (int(x) for x in engine.read(res, 2, np.uint64))
+    finally:
+        res.free()
+    assert hits == 0
+    return cnt
+
+
+@pytest.mark.parametrize("which,expected", [("16", 7309), ("15", 3481026)])
+def test_two_stage_count_simulated_ranks(engine, which, expected):
+    """the world > 1 default of shard.sharded_count on the device, every rank's share
+    run in turn on one GPU: replicated frontier_build(1024 W), frontier_refine(r, W, T), count of
+    the refined frontier, replicated-stage leaves on rank 0 only, refinement leaves per rank."""
+    s1 = synth.SEEDS17["S1"]
+    board = synth.parse(s1[:-9] + ("000800000" if which == "16" else "0" * 9))
+    for world in (2, 3, 8):
+        total = 0
+        for r in range(world):
+            size, leaves0 = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT, target=1024 * world)
+            mine, leaves1 = engine.frontier_refine(r, world, 20_000)
+            total += _count_all(engine, mine) + leaves1 + (leaves0 if r == 0 else 0)
+        assert total == expected, (which, world)
+
+
+def test_frontier_rejected_level_leaves_not_counted(engine):
+    """a level whose children exceed the frontier buffer is rejected and the frontier
+    stays at its parents; the solved leaves that level met must not be counted too (they are
+    still below the parents).  Large targets on the 14-clue board force rejections."""
+    s1 = synth.SEEDS17["S1"]
+    b14 = synth.parse(s1[:63] + "000100000" + "0" * 9)
+    for target in (1_000_000, 6_000_000, 30_000_000):
+        size, leaves = engine.frontier_build(b14, mode=L.SDK_FRONTIER_COUNT, target=target)
+        assert _count_all(engine, size) + leaves == 18_204_270, (target, size, leaves)

@@ -211,6 +211,51 @@ def cpu_baseline_python(puzzles, seconds, procs, budget, what):
     }
 
 
+# The reference's own CPU numbers, measured by the survey in the build container (SURVEY §6,
+# BASELINE.md; not published anywhere): quoted beside the GPU figures they compare with.
+REFERENCE_MEASURED = {
+    "solve_17clue": {"value": 0.0059, "unit": "puzzles/s/core",
+                     "how": "DHT_Node.solve_sudoku, -d 0, 5 seeds S1-S5 in 844 core-s (SURVEY §6)"},
+    "check": {"value": 20_400.0, "unit": "boards/s/core",
+              "how": "Sudoku.check intended semantics, _limit_calls disabled, 49 us/board (SURVEY §3.3)"},
+    "post_solve_ms": {"dht": 87.0, "main": 100.0, "unit": "ms",
+                      "how": "wiki 30-clue POST /solve, one node on loopback, -d 0 (SURVEY §3.1)"},
+}
+
+
+def cpu_baseline_check(boards, seconds, procs):
+    """Config C3 on the host: the oracle's line-by-line Python restatement of Sudoku.check
+    (oracle.py_check, sudoku.py:43-94, limiter off) one process per core on disjoint slices of a
+    fixed sample, and the C port (oracle check_batch) with `procs` threads on the whole sample."""
+    import multiprocessing as mp
+    from oracle import oracle as O
+    n = len(boards)
+    per = max(1, -(-n // procs))
+    # a bounded sample: about `seconds` of Python work per process at ~50 us per board
+    per = min(per, max(1000, int(seconds / 50e-6)))
+    slices = [[list(map(int, b)) for b in boards[k * per: min((k + 1) * per, n)]] for k in range(procs)]
+    slices = [sl for sl in slices if sl]
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(len(slices)) as pool:
+        res = pool.map(O.py_check_timed, slices)
+    wall = time.perf_counter() - t0
+    done = sum(r[0] for r in res)
+    busy = max(r[2] for r in res)
+    t1 = time.perf_counter()
+    v = O.check_batch(boards, threads=procs)
+    cwall = time.perf_counter() - t1
+    return {
+        "value": done / busy if busy > 0 else 0.0, "unit": "boards/s", "cores": len(slices), "kind": "port",
+        "per_core": done / busy / len(slices) if busy > 0 else 0.0,
+        "sample": (f"{done} boards of the C3 stream in {len(slices)} disjoint slices, one process per core, "
+                   f"pure-Python Sudoku.check restatement (oracle/oracle.py py_check, sudoku.py:43-94, "
+                   f"limiter off), {busy:.1f} s per process ({wall:.1f} s incl. process start)"),
+        "c_port": {"value": n / cwall, "unit": "boards/s", "threads": procs, "boards": n,
+                   "valid": int((v & 1).sum())},
+        "reference_measured": REFERENCE_MEASURED["check"],
+    }
+
+
 def c2_leg(eng, d, args, synth):
     """Config C2: ~30-clue unique puzzles, resident in HBM, one launch per step."""
     n = args.c2_puzzles
@@ -405,15 +450,16 @@ def lane_dfs_leg(eng, args, synth, L):
                                 "puzzles_per_s": m / cwall, "sample": m}}
 
 
-def http_leg(requests):
+def http_leg(requests, api="dht"):
     """Config C1: one puzzle POSTed to a single node's /solve (wiki 30-clue puzzle), end to end
-    over loopback HTTP, on a GPU-backed node (distributed_sudoku_solver_amd.node)."""
+    over loopback HTTP, on a GPU-backed node (distributed_sudoku_solver_amd.node) serving
+    DHT_Node.py's HTTP surface (api="dht") or main.py's (api="main", main.py:356-375)."""
     import urllib.request
     from distributed_sudoku_solver_amd import synth
     from distributed_sudoku_solver_amd.engine import SudokuEngine
     from distributed_sudoku_solver_amd.node import SudokuNode
     eng = SudokuEngine(0)
-    node = SudokuNode("127.0.0.1", 0, 0, engine=eng, delay_ms=0).start()
+    node = SudokuNode("127.0.0.1", 0, 0, engine=eng, delay_ms=0, api=api).start()
     grid = [[int(c) for c in synth.WIKI[9 * r: 9 * r + 9]] for r in range(9)]
     body = json.dumps({"sudoku": grid}).encode()
     lat, ok = [], True
@@ -429,10 +475,11 @@ def http_leg(requests):
         node.stop(graceful=False)
         eng.close()
     lat = sorted(lat[2:])
-    return {"workload": "C1: wiki 30-clue puzzle POSTed to /solve on one node (loopback HTTP)",
+    ref = "DHT_Node.py" if api == "dht" else "main.py"
+    return {"workload": f"C1: wiki 30-clue puzzle POSTed to /solve on one node, {ref} HTTP surface (loopback)",
             "median_ms": 1000 * lat[len(lat) // 2], "min_ms": 1000 * lat[0], "requests": len(lat),
-            "solution_ok": bool(ok), "reference_ms": 87.0,
-            "reference_note": "DHT_Node.py single node, -d 0, measured in the build container (SURVEY §3.1)"}
+            "solution_ok": bool(ok), "reference_ms": REFERENCE_MEASURED["post_solve_ms"][api],
+            "reference_note": f"{ref} single node, -d 0, measured in the build container (SURVEY §3.1)"}
 
 
 def launch_ranks(args):
@@ -571,6 +618,9 @@ def main():
                          "kernel": "sdk::check_kernel"},
             "parity": {"mismatched_boards": cbad, "checked_boards": d.world * nb},
         }
+        if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
+            checker_leg["cpu_baseline"] = cpu_baseline_check(pool[:1_000_000], min(5.0, args.cpu_seconds),
+                                                             args.cpu_cores or cpu_share())
 
     # ------------------------------------------------- C4 solve (headline)
     total = args.batch
@@ -699,10 +749,12 @@ def main():
         # fixed C4 sample: the first 8 puzzles of every core's slice are the same on every run
         result["cpu_baseline"] = cpu_baseline_python(puzzles[:cores * 64], args.cpu_seconds, cores,
                                                      args.cpu_puzzle_budget, "C4 17-clue sample")
+        result["cpu_baseline"]["reference_measured"] = REFERENCE_MEASURED["solve_17clue"]
         result["cpu_baseline_c_port"] = cpu_baseline_c(puzzles, args.cpu_seconds, cores)
 
     if d.rank == 0 and d.world == 1 and args.http_requests > 0:
         side("post_solve_latency", lambda: http_leg(args.http_requests))
+        side("post_solve_latency_main", lambda: http_leg(args.http_requests, api="main"))
 
     # -------------------------------------------- per-lane reference DFS (north star part 3)
     if d.rank == 0 and d.world == 1 and args.lane_puzzles > 0:

@@ -66,14 +66,14 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 import numpy as np
 
 from .engine import ALL_DIGITS_MASK, encode_solve_grid, range_to_mask
-from .search import DEFAULT_BUDGET, DEFAULT_MAX_PENDING, DEFAULT_WIDTH, LexSearch
+from .search import DEFAULT_MAX_PENDING, DEFAULT_WIDTH, LexSearch, default_budget
 from .utils import split_array_in_middle
 from . import _lib as L
 
 RECV_BYTES = 1024          # DHT_Node.py:82,94
 HEARTBEAT_S = 5.0          # DHT_Node.py:43
 STATS_WAIT_S = 1.0         # DHT_Node.py:571
-SEARCH_LIMIT_S = 30.0      # a budget-hit task's continued search gives up after this (EXHAUSTED)
+SEARCH_LIMIT_S = 10.0      # a budget-hit task's continued search gives up after this (EXHAUSTED)
 DONE_UUIDS_KEPT = 1 << 16  # answered puzzles remembered (late duplicates are dropped)
 
 
@@ -134,7 +134,7 @@ class SudokuNode:
 
     def __init__(self, host, p2p_port, http_port, anchor=None, engine=None, delay_ms=0.0,
                  heartbeat_s=HEARTBEAT_S, stats_wait_s=STATS_WAIT_S, solve_timeout_s=600.0, log=False,
-                 api="dht", split=True, trace=False, node_budget=DEFAULT_BUDGET, search_limit_s=SEARCH_LIMIT_S,
+                 api="dht", split=True, trace=False, node_budget=None, search_limit_s=SEARCH_LIMIT_S,
                  search_width=DEFAULT_WIDTH, search_max_pending=DEFAULT_MAX_PENDING):
         if api not in ("dht", "main"):
             raise ValueError("api must be 'dht' (DHT_Node.py) or 'main' (main.py)")
@@ -149,9 +149,9 @@ class SudokuNode:
         self.heartbeat_s = heartbeat_s
         self.stats_wait_s = stats_wait_s
         self.solve_timeout_s = solve_timeout_s
-        if node_budget < 1:
+        if node_budget is not None and node_budget < 1:
             raise ValueError("node_budget must be >= 1: an unbounded launch can hold the GPU forever")
-        self.node_budget = int(node_budget)
+        self._node_budget = None if node_budget is None else int(node_budget)
         self.search_limit_s = float(search_limit_s)
         self.search_width = int(search_width)
         self.search_max_pending = int(search_max_pending)
@@ -160,6 +160,7 @@ class SudokuNode:
             from .solver import default_engine
             engine = default_engine()
         self.engine = engine
+        self.node_budget = self._node_budget or default_budget(engine)   # per board per launch
         # ring state (guarded by self.lock)
         self.lock = threading.RLock()
         self.network = []

@@ -17,6 +17,10 @@ product-path solve here is bounded:
     digits ascending -- after propagation, one batched call on the GPU).  The first
     SOLVED sub-board whose predecessors are all refuted holds the reference's answer
     (its lex-first completion); later sub-boards are dropped as soon as one solves.
+    Only the first width/EXPAND_SHARE hits of a slice are expanded (the front of the lex
+    order, where the answer is decided first); later hits go back unexpanded, and when
+    most of a slice hits, the budget doubles (up to `max_budget`) -- so the worklist
+    grows by about one slice per slice instead of nine.
   * the worklist only ever goes deeper, so the search ends on every board the engine
     can finish; a board whose worklist outgrows `max_pending` sub-boards, or whose caller's
     deadline passes, ends as SDK_BUDGET_HIT ("search exhausted"): a defined answer that
@@ -38,6 +42,19 @@ from .engine import ALL_DIGITS_MASK
 DEFAULT_BUDGET = 2048          # search nodes per board per launch (a ~10 ms bound on MI355X)
 DEFAULT_WIDTH = 16384          # sub-boards per slice (fills the solver's resident slots)
 DEFAULT_MAX_PENDING = 1 << 20  # sub-boards the worklist may hold (81 MB of host memory)
+BUDGET_GROWTH_CAP = 8          # the per-launch budget may double up to this multiple of the first
+EXPAND_SHARE = 32              # a slice expands at most width / this of its hits (the lex front)
+LANE_VALIDATIONS_PER_NODE = 4096   # SDK_SOLVER_LANE budgets count the reference's validations
+
+
+def default_budget(engine):
+    """Per-launch budget for `engine`: DEFAULT_BUDGET search nodes, or as many of the reference's
+    validations for the per-lane reference DFS (SDK_SOLVER_LANE counts its budget in those)."""
+    try:
+        lane = engine.get_option(L.SDK_OPT_SOLVER) == L.SDK_SOLVER_LANE
+    except (AttributeError, KeyError, L.SudokuHipError):
+        lane = False
+    return DEFAULT_BUDGET * (LANE_VALIDATIONS_PER_NODE if lane else 1)
 
 
 class LexSearch:
@@ -54,12 +71,13 @@ class LexSearch:
     (exhausted: the worklist outgrew max_pending, or run()'s deadline passed)."""
 
     def __init__(self, engine, board, mask=None, budget=DEFAULT_BUDGET, width=DEFAULT_WIDTH,
-                 max_pending=DEFAULT_MAX_PENDING, hit=False):
+                 max_pending=DEFAULT_MAX_PENDING, hit=False, max_budget=None):
         if budget < 1 or width < 1:
             raise ValueError("budget and width must be >= 1")
         self.engine = engine
         self.input = np.ascontiguousarray(board, dtype=np.uint8).reshape(81).copy()
         self.budget = int(budget)
+        self.max_budget = max(self.budget, int(max_budget) if max_budget else BUDGET_GROWTH_CAP * self.budget)
         self.width = int(width)
         self.max_pending = int(max_pending)
         root_mask = ALL_DIGITS_MASK if mask is None else int(mask)
@@ -147,7 +165,11 @@ class LexSearch:
             self._chunks.clear()
             self._pending = 0
         if len(hits):
-            self._push_front(*self._expand(boards[hits], masks[hits]))
+            k = min(len(hits), max(1, self.width // EXPAND_SHARE))
+            self._push_front(boards[hits[k:]], masks[hits[k:]])           # retried later, unexpanded
+            self._push_front(*self._expand(boards[hits[:k]], masks[hits[:k]]))
+            if 2 * len(hits) > len(boards):
+                self.budget = min(2 * self.budget, self.max_budget)
         if self._pending == 0:
             self._finish(L.SDK_SOLVED if self.best is not None else L.SDK_UNSOLVABLE)
             return True
@@ -166,7 +188,7 @@ class LexSearch:
 
 
 def solve_bounded(engine, boards, masks=None, budget=DEFAULT_BUDGET, time_limit=None, width=DEFAULT_WIDTH,
-                  max_pending=DEFAULT_MAX_PENDING):
+                  max_pending=DEFAULT_MAX_PENDING, max_budget=None):
     """solve_batch with every board bounded: one launch at `budget` nodes per board, then a
     LexSearch per board that hit it, each until done or `time_limit` seconds (None = no limit).
     Returns (out, status, work) like solve_batch; status SDK_BUDGET_HIT = search exhausted."""
@@ -176,7 +198,8 @@ def solve_bounded(engine, boards, masks=None, budget=DEFAULT_BUDGET, time_limit=
     work = np.zeros(len(boards), np.uint64) if work is None else np.array(work, dtype=np.uint64)
     for i in np.flatnonzero(st == L.SDK_BUDGET_HIT):
         m = None if masks is None else int(np.asarray(masks)[i])
-        s = LexSearch(engine, boards[i], m, budget=budget, width=width, max_pending=max_pending, hit=True)
+        s = LexSearch(engine, boards[i], m, budget=budget, width=width, max_pending=max_pending, hit=True,
+                      max_budget=max_budget)
         s.run(None if time_limit is None else time.monotonic() + time_limit)
         out[i], st[i] = s.board, s.status
         work[i] += np.uint64(s.nodes)

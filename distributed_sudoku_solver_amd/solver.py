@@ -32,7 +32,7 @@ import time
 import numpy as np
 
 from .engine import SudokuEngine, encode_solve_grid, range_to_mask
-from .search import DEFAULT_BUDGET, LexSearch
+from .search import DEFAULT_BUDGET, LexSearch, default_budget
 from .utils import split_array_in_middle
 from . import _lib as L
 
@@ -59,13 +59,14 @@ def _empty_cells(puzzle):
     return [(r, c) for r in range(9) for c in range(9) if puzzle[r][c] == 0]
 
 
-def solve_grid(puzzle, arr=range(1, 10), engine=None, budget=DEFAULT_BUDGET, time_limit=DEFAULT_TIME_LIMIT_S):
+def solve_grid(puzzle, arr=range(1, 10), engine=None, budget=None, time_limit=DEFAULT_TIME_LIMIT_S):
     """Core drop-in: mutate `puzzle` like the reference solver and return (ok, work).
 
-    Bounded (module docstring): raises SearchExhausted when the search gives up."""
+    Bounded (module docstring): raises SearchExhausted when the search gives up.  budget =
+    per-launch budget (None: search.default_budget of the engine)."""
     eng = engine or default_engine()
     board = encode_solve_grid(puzzle)
-    search = LexSearch(eng, board, range_to_mask(arr), budget=budget)
+    search = LexSearch(eng, board, range_to_mask(arr), budget=default_budget(eng) if budget is None else budget)
     st, sol = search.run(None if time_limit is None else time.monotonic() + time_limit)
     if st == L.SDK_BUDGET_HIT:
         raise SearchExhausted(f"search exhausted after {search.nodes} nodes in {search.launches} launches; "

@@ -198,3 +198,14 @@ def py_solve_timed(boards, seconds, budget=0):
         solved += int(bool(ok))
         timeouts += int(ok is None)
     return done, solved, time.perf_counter() - t0, timeouts
+
+
+def py_check_timed(boards):
+    """Baseline worker (bench.py checker cpu_baseline): py_check over `boards` (81-int lists).
+    Returns (boards checked, intended-valid count, wall seconds)."""
+    import time
+    t0 = time.perf_counter()
+    ok = 0
+    for cells in boards:
+        ok += int(py_check(cells)[1])
+    return len(boards), ok, time.perf_counter() - t0

@@ -184,3 +184,21 @@ def test_split_with_budget_hit_lower_half_on_gpu(engine):
             assert "".join(str(v) for row in body["solution"] for v in row) == synth.SEED_SOLUTIONS[name]
     finally:
         _stop([a, b])
+
+
+# ------------------------------------------------------- failure re-execution
+def test_crashed_neighbour_half_rerun_on_gpu(engine):
+    """HIP origin A hands range(5, 10) of S1 (where its answer lies) to B, B
+    crashes without NODE_FAILED, A detects it by heartbeat, re-runs the half on the GPU and the POST
+    returns the reference's board (DHT_Node.py:158-209)."""
+    from test_node import OracleEngine, failure_rerun_scenario
+    failure_rerun_scenario(engine, OracleEngine())
+    failure_rerun_scenario(engine, engine)            # both nodes on the HIP engine
+
+
+def test_graceful_stop_hands_queue_back_on_gpu(engine):
+    """a node stopping gracefully hands its queued task to its neighbour, the
+    HIP origin, which answers golden (DHT_Node.py:137-156)."""
+    from test_node import OracleEngine, graceful_stop_scenario
+    graceful_stop_scenario(OracleEngine(), engine)
+    graceful_stop_scenario(engine, engine)

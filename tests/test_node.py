@@ -563,3 +563,87 @@ def test_exhausted_lower_range_blocks_upper_completion():
     finally:
         node.httpd.server_close()
         node.sock.close()
+
+
+# ------------------------------------------------------- failure re-execution
+def failure_rerun_scenario(engine_a, engine_b):
+    """DHT_Node.py:158-209: A (the HTTP origin) splits S1, keeping range(1, 5) -- no completion there
+    -- and handing range(5, 10) -- the answer -- to B.  B crashes (no NODE_FAILED) before solving
+    it; A's heartbeat check finds B dead, re-runs the delegated half itself (neighbor_tasks) and
+    the POST returns the reference's answer.  Returns A's trace."""
+    a = SudokuNode("127.0.0.1", 0, 0, engine=engine_a, delay_ms=0, trace=True, heartbeat_s=0.2).start()
+    b = SudokuNode("127.0.0.1", 0, 0, anchor=a.me, engine=engine_b, delay_ms=0, trace=True, heartbeat_s=0.2).start()
+    try:
+        assert b.wait_joined()
+        t0 = time.time()
+        while not a.neighborfree and time.time() - t0 < 10:
+            time.sleep(0.01)
+        assert a.neighborfree
+        b.pause()                                          # B queues the half it gets and never runs it
+        import threading
+        res = {}
+        th = threading.Thread(target=lambda: res.__setitem__("r", _post(a.http_port, _grid(synth.SEEDS17["S1"]))))
+        th.start()
+        while b.tasks.qsize() < 1 and time.time() - t0 < 10:
+            time.sleep(0.01)
+        assert b.tasks.qsize() == 1 and not res                 # B holds range(5, 10); nothing answered yet
+        b.stop(graceful=False)                             # crash
+        th.join(30)
+        code, body = res["r"]
+        assert code == 201
+        assert "".join(str(v) for row in body["solution"] for v in row) == synth.SEED_SOLUTIONS["S1"]
+        assert b.me not in a.network and a.neighbor == a.me
+        sent = [t for t in a.trace if t[0] == "TASK"]
+        assert sent[0][1:] == (b.me, range(5, 10))
+        return a
+    finally:
+        _stop([a, b])
+
+
+def graceful_stop_scenario(engine_a, engine_b):
+    """DHT_Node.py:137-156: B (the HTTP origin, busy) hands a task to its free neighbour A; A stops
+    gracefully before running it: its queued task goes back to its neighbour and NODE_FAILED to
+    the coordinator, and the POST on B still answers the reference's board."""
+    b = SudokuNode("127.0.0.1", 0, 0, engine=engine_b, delay_ms=0, trace=True, split=False).start()
+    a = SudokuNode("127.0.0.1", 0, 0, anchor=b.me, engine=engine_a, delay_ms=0, trace=True, split=False).start()
+    try:
+        assert a.wait_joined()
+        t0 = time.time()
+        while not b.neighborfree and time.time() - t0 < 10:
+            time.sleep(0.01)
+        assert b.neighborfree
+        a.pause()
+        with b.lock:
+            b.busy = True                                  # B busy: a new task goes to the free neighbour
+        import threading
+        res = {}
+        th = threading.Thread(target=lambda: res.__setitem__("r", _post(b.http_port, _grid(synth.SEEDS17["S2"]))))
+        th.start()
+        while a.tasks.qsize() < 1 and time.time() - t0 < 10:
+            time.sleep(0.01)
+        assert a.tasks.qsize() == 1
+        a.stop(graceful=True)
+        with b.lock:
+            b.busy = False
+        with b._work:
+            b._work.notify()
+        th.join(30)
+        code, body = res["r"]
+        assert code == 201
+        assert "".join(str(v) for row in body["solution"] for v in row) == synth.SEED_SOLUTIONS["S2"]
+        assert any(t[0] == "TASK" and t[1] == b.me for t in a.trace)          # handed back
+        assert any(t[0] == "NODE_FAILED" and t[1] == b.me for t in a.trace)   # coordinator told
+        t0 = time.time()
+        while a.me in b.network and time.time() - t0 < 5:
+            time.sleep(0.01)
+        assert b.network == [b.me]
+    finally:
+        _stop([a, b])
+
+
+def test_failure_reruns_delegated_half():
+    failure_rerun_scenario(OracleEngine(), OracleEngine())
+
+
+def test_graceful_stop_hands_queue_to_neighbour():
+    graceful_stop_scenario(OracleEngine(), OracleEngine())

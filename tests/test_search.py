@@ -2,6 +2,8 @@
 on the oracle double: whatever the node budget, the answer is the reference's (golden vectors
 made by importing the reference, DHT_Node.py:474-538), and a board no budget finishes ends as
 SDK_BUDGET_HIT, never as "no solution".  tests/test_gpu_search.py runs the same on the GPU."""
+import time
+
 import numpy as np
 import pytest
 
@@ -47,11 +49,11 @@ def test_lex_search_continues_budget_hits(solve_cases):
 
 def test_exhausted_is_not_unsolvable():
     eng = OracleEngine()
-    s = LexSearch(eng, synth.parse(CONFLICT55), budget=1, width=32, max_pending=2000)
-    st, out = s.run()
+    s = LexSearch(eng, synth.parse(CONFLICT55), budget=1, width=32, max_pending=200, max_budget=1)
+    st, out = s.run(time.monotonic() + 60)
+    assert s.pending == 0 and s.expansions > 1
     assert st == L.SDK_BUDGET_HIT and out.tolist() == synth.parse(CONFLICT55).tolist()
     s = LexSearch(eng, synth.parse(CONFLICT55), budget=1, width=32)
-    import time
     st, _ = s.run(deadline=time.monotonic() + 0.5)
     assert st == L.SDK_BUDGET_HIT
 

@@ -73,6 +73,7 @@ from . import _lib as L
 RECV_BYTES = 1024          # DHT_Node.py:82,94
 HEARTBEAT_S = 5.0          # DHT_Node.py:43
 STATS_WAIT_S = 1.0         # DHT_Node.py:571
+SLICE_TARGET_S = 0.01     # wall time of one search slice's launch (search.LexSearch slice_target_s)
 SEARCH_LIMIT_S = 10.0      # a budget-hit task's continued search gives up after this (EXHAUSTED)
 DONE_UUIDS_KEPT = 1 << 16  # answered puzzles remembered (late duplicates are dropped)
 
@@ -553,7 +554,7 @@ class SudokuNode:
             if st == L.SDK_BUDGET_HIT:
                 # not "no solution": the subtree is unexplored.  Continue it alone, between batches
                 s = LexSearch(self.engine, b, int(m), budget=self.node_budget, width=self.search_width,
-                              max_pending=self.search_max_pending, hit=True)
+                              max_pending=self.search_max_pending, hit=True, slice_target_s=SLICE_TARGET_S)
                 with self.lock:
                     self.hard.append(_HardTask(t, s, time.monotonic() + self.search_limit_s))
                 self._log("budget hit, continuing", t.get("uuid"))

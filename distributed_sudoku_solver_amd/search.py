@@ -71,7 +71,7 @@ class LexSearch:
     (exhausted: the worklist outgrew max_pending, or run()'s deadline passed)."""
 
     def __init__(self, engine, board, mask=None, budget=DEFAULT_BUDGET, width=DEFAULT_WIDTH,
-                 max_pending=DEFAULT_MAX_PENDING, hit=False, max_budget=None):
+                 max_pending=DEFAULT_MAX_PENDING, hit=False, max_budget=None, slice_target_s=None):
         if budget < 1 or width < 1:
             raise ValueError("budget and width must be >= 1")
         self.engine = engine
@@ -79,6 +79,12 @@ class LexSearch:
         self.budget = int(budget)
         self.max_budget = max(self.budget, int(max_budget) if max_budget else BUDGET_GROWTH_CAP * self.budget)
         self.width = int(width)
+        # wall-time target of one slice's launch (None: no target).  A launch over it halves the
+        # budget (down to 1/BUDGET_GROWTH_CAP of the first), and the budget only grows while
+        # launches stay under half of it -- so a node's worker never waits on a search slice
+        # much longer than this between two batches of new puzzles.
+        self.slice_target_s = None if slice_target_s is None else float(slice_target_s)
+        self.min_budget = max(1, self.budget // BUDGET_GROWTH_CAP)
         self.max_pending = int(max_pending)
         root_mask = ALL_DIGITS_MASK if mask is None else int(mask)
         # worklist: chunks (boards uint8[k,81], masks uint16[k]) in lex order of their subtrees
@@ -150,7 +156,9 @@ class LexSearch:
             self._finish(L.SDK_SOLVED if self.best is not None else L.SDK_UNSOLVABLE)
             return True
         boards, masks = self._take(self.width)
+        t0 = time.monotonic()
         out, st, work = self.engine.solve_batch(boards, masks, want_work=True, budget=self.budget)
+        elapsed = time.monotonic() - t0
         self.launches += 1
         if work is not None:
             self.nodes += int(np.asarray(work, dtype=np.uint64).sum())
@@ -168,7 +176,11 @@ class LexSearch:
             k = min(len(hits), max(1, self.width // EXPAND_SHARE))
             self._push_front(boards[hits[k:]], masks[hits[k:]])           # retried later, unexpanded
             self._push_front(*self._expand(boards[hits[:k]], masks[hits[:k]]))
-            if 2 * len(hits) > len(boards):
+            slow = self.slice_target_s is not None and elapsed > self.slice_target_s
+            fast = self.slice_target_s is None or 2 * elapsed < self.slice_target_s
+            if slow:
+                self.budget = max(self.min_budget, self.budget // 2)
+            elif fast and 2 * len(hits) > len(boards):
                 self.budget = min(2 * self.budget, self.max_budget)
         if self._pending == 0:
             self._finish(L.SDK_SOLVED if self.best is not None else L.SDK_UNSOLVABLE)

@@ -39,6 +39,9 @@ SDK_OPT_TIMING = 11
 SDK_OPT_TIMER_EVENTS = 12
 SDK_OPT_LOCKED = 13
 SDK_OPT_XCD_HEADS = 14
+SDK_OPT_DONATE = 15
+SDK_OPT_DONATED = 16
+SDK_OPT_SPLIT_BOARDS = 17
 SDK_CHECK_REG1 = 0
 SDK_CHECK_REG2 = 1
 SDK_CHECK_GLDS2 = 2

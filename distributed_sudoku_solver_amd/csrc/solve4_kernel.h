@@ -493,7 +493,492 @@ struct Args4 : Args2 {
     uint32_t count_lim;       // per-board stop: the count limit, or the flush point 2^31
     bool count_stop;          // count_lim is the caller's limit (stop there), not a flush point
     unsigned long long* count;
+    // subtree donation (solve4_kernel<true>, see below): control block, then records, items,
+    // registrations and mailboxes at fixed offsets
+    struct DnCtl* dn;
 };
+
+// ------------------------------------------------------------------ subtree donation
+// solve4_kernel<true> (SDK_OPT_DONATE, LEX solves): the reference splits a running search
+// at any depth and hands the other half to a free node (DHT_Node.py:491-510).  Here a
+// board that has searched kDnEvery more nodes while whole waves sit idle at the end of
+// the launch gives away the highest untried digits of its SHALLOWEST stack level -- the
+// largest untried subtrees and the lex-greatest part of its remaining search -- as
+// "items": the level's propagated state with the branch cell set to one digit each (216 B
+// in the lane layout).  Each item goes straight to one idle wave, which searches it like
+// a board (a "part" of the board); a part can donate again.
+//
+// Lex-first answer (ordered acceptance).  In LEX order every cell before a node's branch
+// cell is closed, so a part's completions all start with its root prefix: the digits of
+// cells 0..cell (plen = cell + 1) of its root; the donor keeps only completions below
+// every donated prefix.  Each part stops at its own first completion (its region's
+// lex-first one).  A part whose prefix is above some completion already found can hold no
+// better one and stops (pruned).  When the last part of a board ends, the finisher
+// writes the smallest completion found -- the board's lex-first completion, the
+// reference's answer -- unless a part that hit the node budget could still hold a
+// smaller one (then SDK_BUDGET_HIT, as for an undonated board).  Only boards whose units
+// are all exact donate (no duplicated or inert given: every closed cell is a digit).
+//
+// Hand-off without a shared queue word: a wave whose four slots are idle counts itself
+// in `finished`, registers its id once (reg[reg_tail++]) and polls only its own mailbox.
+// A donor takes registrations (reg_head += k, at most as many as are registered), takes
+// each receiver out of `finished` and stores the item index in its mailbox.  A wave leaves
+// when every wave of the grid is counted idle: no part is running, so no item can be on
+// its way (receivers are un-counted by their donor before the delivery).  Registrations a
+// donor reserved but could not use are simply never served.  The counters and registries
+// are kept per XCD (workgroup % 8, the dispatch's round robin), each on its own cache
+// line: thousands of waves go idle at once when the launch starts or drains, and one
+// shared counter would serialise their atomics; a donor serves its own XCD's idle waves
+// first (the item it writes is then in that XCD's L2).
+constexpr int kDnXcds = 8;
+struct DnXcd {
+    uint32_t finished;        // waves of this XCD counted idle
+    uint32_t reg_tail;        // registrations of idle waves
+    uint32_t reg_head;        // registrations taken by donors
+    uint32_t pad[29];
+};
+struct DnCtl {
+    uint32_t epoch;           // launch number (host): mailbox and registration entries carry it
+    uint32_t item_alloc;      // item records handed out
+    uint32_t nrec;            // board records handed out
+    uint32_t delivered, exit_all, parts_ended, finalized;   // diagnostics
+    uint32_t pad[25];
+    DnXcd x[kDnXcds];
+};
+constexpr uint32_t kDnItems = 1u << 16;
+constexpr uint32_t kDnRecs = 1u << 14;
+constexpr uint32_t kDnRegX = 1u << 14;        // registrations per XCD
+constexpr uint32_t kDnReg = kDnRegX * kDnXcds;
+constexpr uint32_t kDnMbox = 1u << 14;        // workgroups of a donating launch, at most
+constexpr int kDnList = 16;
+constexpr uint32_t kDnNone = 0xFFFFFFFFu, kDnOwner = 0xFFFFFFFEu;
+#ifndef SDK_DN_EVERY
+#define SDK_DN_EVERY 64
+#endif
+constexpr uint32_t kDnEvery = SDK_DN_EVERY;   // nodes between a part's donation / pruning checks
+#ifndef SDK_DN_SLEEP
+// s_sleep argument between an idle wave's mailbox polls (x 64 clocks: ~3.4 us).  Shorter
+// sleeps let the ~23 idle waves of a CU take issue slots and memory bandwidth from the one
+// that still searches (s_sleep 4: the 64 heaviest hard boards 1.5 -> 9.7 ms).
+#define SDK_DN_SLEEP 127
+#endif
+constexpr int kDnPruned = 3;                  // part status: stopped above a known completion
+struct DnItem {
+    uint32_t board, rec, plen, pad0;
+    uint32_t pad[4];
+    uint2 w[27];              // root state, lane j: (y0 | y1 << 16, y2), snapshot encoding
+    uint8_t sol[96];          // the part's completion
+    uint32_t pad2[10];
+};
+struct DnRec {                // one per donating board
+    uint32_t board, open, nsol, nhit, flags, maxd;
+    unsigned long long work;
+    uint32_t sol[kDnList];    // parts that found a completion (kDnOwner: the board's own slot)
+    uint32_t hit[kDnList];    // parts that hit the node budget
+    uint8_t owner_sol[96];
+};
+static_assert(sizeof(DnItem) == 384 && sizeof(DnRec) == 256 && sizeof(DnCtl) == 128 * (1 + kDnXcds), "donation layout");
+constexpr size_t kDnRecOffset = sizeof(DnCtl);
+constexpr size_t kDnItemOffset = kDnRecOffset + (size_t)kDnRecs * sizeof(DnRec);
+constexpr size_t kDnRegOffset = kDnItemOffset + (size_t)kDnItems * sizeof(DnItem);
+constexpr size_t kDnMboxOffset = kDnRegOffset + (size_t)kDnReg * 8;
+constexpr size_t kDnBytes = kDnMboxOffset + (size_t)kDnMbox * 8;
+__device__ __forceinline__ DnRec* dn_recs4(const Args4& a) {
+    return reinterpret_cast<DnRec*>(reinterpret_cast<char*>(a.dn) + kDnRecOffset);
+}
+__device__ __forceinline__ DnItem* dn_items4(const Args4& a) {
+    return reinterpret_cast<DnItem*>(reinterpret_cast<char*>(a.dn) + kDnItemOffset);
+}
+__device__ __forceinline__ unsigned long long* dn_reg4(const Args4& a) {
+    return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.dn) + kDnRegOffset);
+}
+__device__ __forceinline__ unsigned long long* dn_mbox4(const Args4& a) {
+    return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.dn) + kDnMboxOffset);
+}
+struct SlotDn {
+    uint32_t rec, part, base, plen;   // record, part id (item / kDnOwner), first live stack level,
+                                      // prefix length (bit 31: pruned, end the part at its next step)
+};
+constexpr uint32_t kDnAbort = 0x80000000u;
+// a part that ended, waiting for its bookkeeping (dn_finish_part4, run once per loop
+// iteration: inlined at one place instead of at every end of a search step)
+struct DnFin {
+    uint32_t rec, part;
+    int st;
+    uint32_t maxd;
+    unsigned long long work;
+};
+static __shared__ SlotDn s_dn4[4];    // per slot (half * 2 + slot); referenced by solve4_kernel<true> only
+static __shared__ DnFin s_dnfin4[4];
+static __shared__ uint32_t s_dnpend4; // bit k: s_dnfin4[k] waits; bit 4 + k: slot k's check is due
+static __shared__ uint32_t s_dnwave4; // bit 0: counted in `finished`, bit 1: registered, bits 8..: polls
+static __shared__ uint32_t s_dnepoch4;
+
+// runtime-slot field access (the donation paths run once per loop iteration for any slot)
+__device__ __forceinline__ uint32_t fld_rt(uint32_t w, uint32_t hi) {
+    return hi ? (w >> 16) : (w & 0xFFFFu);
+}
+__device__ __forceinline__ uint32_t setfld_rt(uint32_t w, uint32_t v, uint32_t hi) {
+    return hi ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_agent64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// digit of a closed cell in the 16-bit snapshot encoding (S | 0x400 with S = 1 << (digit-1))
+__device__ __forceinline__ uint32_t snap_digit4(uint32_t y) {
+    return (uint32_t)__ffs(y & 0x1FFu);
+}
+// A[:L] < B[:L] lexicographically, per 32-lane half; a*, b* = the lane's digits of cells
+// c0, c0 + 27, c0 + 54 (every cell index < 81, so three ballots order all cells)
+__device__ __forceinline__ bool half_less4(const Lane4& w, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t b0,
+                                           uint32_t b1, uint32_t b2, int L) {
+    const bool d0 = w.act && w.c0 < L && a0 != b0;
+    const bool d1 = w.act && w.c0 + 27 < L && a1 != b1;
+    const bool d2 = w.act && w.c0 + 54 < L && a2 != b2;
+    const uint64_t D0 = __ballot(d0), D1 = __ballot(d1), D2 = __ballot(d2);
+    const uint64_t L0 = __ballot(d0 && a0 < b0), L1 = __ballot(d1 && a1 < b1), L2 = __ballot(d2 && a2 < b2);
+    const int sh = 32 * w.half;
+    const uint32_t e0 = (uint32_t)(D0 >> sh), e1 = (uint32_t)(D1 >> sh), e2 = (uint32_t)(D2 >> sh);
+    const uint32_t l0 = (uint32_t)(L0 >> sh), l1 = (uint32_t)(L1 >> sh), l2 = (uint32_t)(L2 >> sh);
+    if (e0) return (l0 >> __builtin_ctz(e0)) & 1u;
+    if (e1) return (l1 >> __builtin_ctz(e1)) & 1u;
+    if (e2) return (l2 >> __builtin_ctz(e2)) & 1u;
+    return false;
+}
+__device__ __forceinline__ const uint8_t* dn_sol4(const Args4& a, const DnRec* r, uint32_t id) {
+    return id == kDnOwner ? r->owner_sol : dn_items4(a)[id].sol;
+}
+// the lane's three digits of an 81-byte completion
+__device__ __forceinline__ void dn_digits4(const Lane4& w, const uint8_t* s, uint32_t& v0, uint32_t& v1, uint32_t& v2) {
+    v0 = w.act ? s[w.c0] : 0u;
+    v1 = w.act ? s[w.c0 + 27] : 0u;
+    v2 = w.act ? s[w.c0 + 54] : 0u;
+}
+// the lane's three root-prefix digits of item `id`
+__device__ __forceinline__ void dn_prefix4(const Lane4& w, const Args4& a, uint32_t id, uint32_t& p0, uint32_t& p1,
+                                           uint32_t& p2) {
+    p0 = p1 = p2 = 0u;
+    if (w.act) {
+        const uint2 v = dn_items4(a)[id].w[w.hl];
+        p0 = snap_digit4(v.x & 0xFFFFu);
+        p1 = snap_digit4(v.x >> 16);
+        p2 = snap_digit4(v.y & 0xFFFFu);
+    }
+}
+
+// an item part: is some completion of its board already below its root prefix?
+__device__ __forceinline__ bool dn_pruned4(const Lane4& w, const Args4& a, const SlotDn& d) {
+    const DnRec* r = dn_recs4(a) + d.rec;
+    const uint32_t ns = min(ld_agent(&r->nsol), (uint32_t)kDnList);
+    if (ns == 0) return false;
+    uint32_t p0, p1, p2;
+    dn_prefix4(w, a, d.part, p0, p1, p2);
+    bool pruned = false;
+    for (uint32_t k = 0; k < ns && !pruned; ++k) {
+        const uint32_t id = ld_agent(&r->sol[k]);
+        if (id == kDnNone) continue;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        uint32_t s0, s1, s2;
+        dn_digits4(w, dn_sol4(a, r, id), s0, s1, s2);
+        pruned = half_less4(w, s0, s1, s2, p0, p1, p2, (int)(d.plen & ~kDnAbort));
+    }
+    return pruned;
+}
+
+// give the highest untried digits of stack level d.base (the shallowest live one) to idle
+// waves, one item each: as many as there are registered idle waves
+__device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const Slot4& b, const Cells4& c,
+                                           uint32_t hi, SlotDn* pd, uint2* g_stk) {
+    DnCtl* ctl = a.dn;
+    const SlotDn d = *pd;
+    if (b.depth <= d.base) return;
+    // the first XCD (from this workgroup's own) with registered idle waves
+    uint32_t x = kDnXcds, tail = 0, head = 0;
+    for (uint32_t k = 0; k < (uint32_t)kDnXcds; ++k) {
+        const uint32_t xx = (blockIdx.x + k) % kDnXcds;
+        tail = ld_agent(&ctl->x[xx].reg_tail);
+        head = ld_agent(&ctl->x[xx].reg_head);
+        if (tail > head && head < kDnRegX) {
+            x = xx;
+            break;
+        }
+    }
+    if (x == kDnXcds) return;                                     // no idle wave waits
+    if (half_any4(w, w.act && fld_rt(c.E, hi) == 0u)) return;   // only boards with every unit exact
+    const uint32_t lvl = d.base;
+    uint2* lp = g_stk + (lvl * 2 + hi) * 64 + w.lane;
+    const uint2 snap = *lp;
+    const uint32_t rec16 = snap.y >> 16;
+    const int cell = (int)(rec16 & 0x7Fu);
+    const uint32_t rest = rec16 >> 7;
+    const uint32_t cnt = (uint32_t)__popc(rest);
+    // registrations: tickets t0 .. t0 + valid - 1 are registered idle waves
+    uint32_t t0 = 0, valid = 0;
+    if (w.hl == 0) {
+        const uint32_t want = min(cnt, tail - head);
+        t0 = atomicAdd(&ctl->x[x].reg_head, want);
+        const uint32_t tail2 = min(ld_agent(&ctl->x[x].reg_tail), kDnRegX);
+        valid = tail2 > t0 ? min(want, tail2 - t0) : 0u;
+    }
+    t0 = half_first4(w, t0);
+    valid = half_first4(w, valid);
+    if (valid == 0) return;
+    // board record (first donation of this board)
+    DnRec* recs = dn_recs4(a);
+    uint32_t r = d.rec;
+    if (r == kDnNone) {
+        uint32_t v = 0;
+        if (w.hl == 0) v = atomicAdd(&ctl->nrec, 1u);
+        r = half_first4(w, v);
+        if (r >= kDnRecs) return;                                 // the tickets stay unserved
+        DnRec* R = recs + r;
+        if (w.hl == 0) {
+            R->board = b.bidx;
+            R->open = 1;
+            R->nsol = R->nhit = R->flags = R->maxd = 0;
+            R->work = 0;
+        }
+        if (w.hl < kDnList) {
+            R->sol[w.hl] = kDnNone;
+            R->hit[w.hl] = kDnNone;
+        }
+        if (w.hl == 0) pd->rec = r;
+    }
+    uint32_t i0 = 0;
+    if (w.hl == 0) {
+        i0 = atomicAdd(&ctl->item_alloc, valid);
+        if (i0 + valid <= kDnItems) atomicAdd(&recs[r].open, valid);
+    }
+    i0 = half_first4(w, i0);
+    if (i0 + valid > kDnItems) return;
+    // the `valid` highest digits of the level go
+    uint32_t gone = rest;
+    for (uint32_t k = valid; k < cnt; ++k) gone &= gone - 1u;       // drop the lowest cnt - valid
+    const uint32_t stay = rest & ~gone;
+    const uint32_t y0 = snap.x & 0xFFFFu, y1 = snap.x >> 16, y2 = snap.y & 0xFFFFu;
+    const bool k0 = w.act && cell == w.c0, k1 = w.act && cell == w.c0 + 27, k2 = w.act && cell == w.c0 + 54;
+    DnItem* items = dn_items4(a);
+    uint32_t g = gone;
+    for (uint32_t k = 0; k < valid; ++k) {
+        const uint32_t dbit = g & (0u - g);
+        g ^= dbit;
+        DnItem* it = items + i0 + k;
+        const uint32_t v = dbit | 0x400u;
+        if (w.act) it->w[w.hl] = make_uint2((k0 ? v : y0) | ((k1 ? v : y1) << 16), k2 ? v : y2);
+        if (w.hl == 0) {
+            it->board = b.bidx;
+            it->rec = r;
+            it->plen = (uint32_t)cell + 1u;
+        }
+    }
+    __threadfence();
+    if (w.hl == 0) {
+        const uint32_t epoch = s_dnepoch4;
+        unsigned long long* reg = dn_reg4(a) + (size_t)x * kDnRegX;
+        unsigned long long* mbox = dn_mbox4(a);
+        for (uint32_t k = 0; k < valid; ++k) {
+            unsigned long long e;
+            while (((e = ld_agent64(reg + t0 + k)) >> 32) != epoch) __builtin_amdgcn_s_sleep(1);
+            atomicSub(&ctl->x[x].finished, 1u);                     // the receiver works from now on
+            __hip_atomic_store(mbox + (uint32_t)e, ((unsigned long long)epoch << 32) | (i0 + k), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        atomicAdd(&ctl->delivered, valid);
+    }
+    // the level keeps its lower untried digits; with none left it is the donor's no more
+    if (stay == 0u) {
+        if (w.hl == 0) pd->base = lvl + 1u;   // the part ends when it backtracks to it
+    } else {
+        lp->y = (snap.y & 0xFFFFu) | (((uint32_t)cell | (stay << 7)) << 16);
+    }
+}
+
+// the last part of a board: write its answer (see above)
+__device__ __forceinline__ void dn_finalize4(const Lane4& w, const Args4& a, const DnRec* r) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t board = ld_agent(&r->board);
+    const uint32_t nsol = ld_agent(&r->nsol), nhit = ld_agent(&r->nhit), flags = ld_agent(&r->flags);
+    const uint32_t ns = min(nsol, (uint32_t)kDnList), nh = min(nhit, (uint32_t)kDnList);
+    bool have = false;
+    uint32_t b0 = 0, b1 = 0, b2 = 0;
+    for (uint32_t k = 0; k < ns; ++k) {
+        uint32_t s0, s1, s2;
+        dn_digits4(w, dn_sol4(a, r, ld_agent(&r->sol[k])), s0, s1, s2);
+        if (!have || half_less4(w, s0, s1, s2, b0, b1, b2, 81)) {
+            b0 = s0;
+            b1 = s1;
+            b2 = s2;
+            have = true;
+        }
+    }
+    bool blocked = flags != 0u;   // a list overflowed: undecided
+    for (uint32_t k = 0; k < nh && !blocked; ++k) {
+        const uint32_t id = ld_agent(&r->hit[k]);
+        if (id == kDnOwner) {
+            blocked = true;       // the board's own part: its region holds the smallest prefixes
+        } else {
+            uint32_t p0, p1, p2;
+            dn_prefix4(w, a, id, p0, p1, p2);
+            blocked = !have || !half_less4(w, b0, b1, b2, p0, p1, p2, (int)dn_items4(a)[id].plen);
+        }
+    }
+    const int st = blocked ? -2 : (have ? 1 : 0);
+    uint8_t* dst = a.out + (uint64_t)board * 81;
+    if (w.act) {
+        if (st == 1) {
+            dst[w.c0] = (uint8_t)b0;
+            dst[w.c0 + 27] = (uint8_t)b1;
+            dst[w.c0 + 54] = (uint8_t)b2;
+        } else {   // the reference restores the grid (DHT_Node.py:535)
+            const uint8_t* src = a.in + (a.in_first + (uint64_t)board * a.in_step) * 81;
+            dst[w.c0] = src[w.c0];
+            dst[w.c0 + 27] = src[w.c0 + 27];
+            dst[w.c0 + 54] = src[w.c0 + 54];
+        }
+    }
+    if (w.hl == 0) {
+        a.status[board] = (int8_t)st;
+        if (a.work)
+            a.work[board] = a.work_rounds == 2 ? (uint64_t)ld_agent(&r->maxd)
+                                               : (uint64_t)ld_agent64(&r->work);
+    }
+}
+
+// a part of a donating board ended (st: 1 completion written to its sol, 0 refuted, -2 budget
+// hit, kDnPruned); the last one to end finalizes the board
+__device__ __forceinline__ void dn_finish_part4(const Lane4& w, const Args4& a, const DnFin& f) {
+    DnRec* r = dn_recs4(a) + f.rec;
+    const int st = f.st;
+    __threadfence();              // this part's completion bytes before its list entry
+    if (w.hl == 0) {
+        if (st == 1 || st == -2) {
+            uint32_t* cnt = st == 1 ? &r->nsol : &r->nhit;
+            const uint32_t k = atomicAdd(cnt, 1u);
+            if (k < (uint32_t)kDnList)
+                __hip_atomic_store((st == 1 ? r->sol : r->hit) + k, f.part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                atomicOr(&r->flags, 1u);
+        }
+        atomicAdd(&r->work, f.work);
+        atomicMax(&r->maxd, f.maxd);
+    }
+    __threadfence();              // list entries and counters before the open count
+    uint32_t old = 0;
+    if (w.hl == 0) {
+        old = atomicSub(&r->open, 1u);
+        atomicAdd(&a.dn->parts_ended, 1u);
+        if (old == 1u) atomicAdd(&a.dn->finalized, 1u);
+    }
+    old = half_first4(w, old);
+    if (old == 1u) dn_finalize4(w, a, r);
+}
+
+// start item `idx` in slot `hi` of this half
+__device__ __forceinline__ void dn_start_item4(const Lane4& w, const Args4& a, Cells4& c, uint32_t hi, uint32_t idx,
+                                               Slot4* s_slot) {
+    const DnItem* it = dn_items4(a) + idx;
+    const uint32_t board = it->board, rec = it->rec, plen = it->plen;
+    uint32_t y0 = 0, y1 = 0, y2 = 0;
+    if (w.act) {
+        const uint2 v = it->w[w.hl];
+        y0 = v.x & 0xFFFFu;
+        y1 = v.x >> 16;
+        y2 = v.y & 0xFFFFu;
+    }
+    c.x0 = setfld_rt(c.x0, w.act ? snap_x4(y0) : 0u, hi);
+    c.x1 = setfld_rt(c.x1, w.act ? snap_x4(y1) : 0u, hi);
+    c.x2 = setfld_rt(c.x2, w.act ? snap_x4(y2) : 0u, hi);
+    c.s0 = setfld_rt(c.s0, w.act ? snap_s4(y0) : kInert4, hi);
+    c.s1 = setfld_rt(c.s1, w.act ? snap_s4(y1) : kInert4, hi);
+    c.s2 = setfld_rt(c.s2, w.act ? snap_s4(y2) : kInert4, hi);
+    c.D = setfld_rt(c.D, kCands, hi);  // donating boards are exact: no duplicated given
+    c.E = setfld_rt(c.E, kCands, hi);
+    Slot4 b;
+    b.bidx = board;
+    b.bend = board + 1u;              // the next dequeue goes to the (drained) shared tail
+    b.depth = 0;
+    b.order = ORDER_LEX;
+    b.count = 0;
+    b.lim = 1;
+    b.rstart = a.iter;
+    b.active = 3u;
+    b.maxd = 0;
+    b.nodes = 0;
+    if (w.hl == 0) {
+        s_slot[w.half * 2 + hi] = b;
+        s_dn4[w.half * 2 + hi] = SlotDn{rec, idx, 0u, plen};
+    }
+}
+
+// slot k's donation / pruning check (its step flagged it): an item part already above a
+// known completion is marked to end at its next step; otherwise donate to idle waves
+__device__ __forceinline__ void dn_check4(const Lane4& w, const Args4& a, const Cells4& c, uint32_t k, Slot4* s_slot,
+                                          uint2* g_stk) {
+    SlotDn* pd = s_dn4 + k;
+    const SlotDn d = *pd;
+    if (d.rec != kDnNone && d.part != kDnOwner) {
+        if (dn_pruned4(w, a, d)) {
+            if (w.hl == 0) pd->plen = d.plen | kDnAbort;
+            return;
+        }
+    }
+    dn_donate4(w, a, s_slot[k], c, k & 1u, pd, g_stk);
+}
+
+// a wave whose four slots are idle: count it idle, register it once, poll its mailbox.
+// Returns 0 to leave (the whole grid idle), 1 to poll again, 2 when an item was started in
+// slot 0 of half 0 (A0 then covers that half).
+__device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& c, uint64_t& A0, Slot4* s_slot) {
+    DnCtl* ctl = a.dn;
+    DnXcd* mx = ctl->x + blockIdx.x % kDnXcds;
+    uint32_t st = __builtin_amdgcn_readfirstlane(s_dnwave4);
+    const uint32_t epoch = __builtin_amdgcn_readfirstlane(s_dnepoch4);
+    unsigned long long* mbox = dn_mbox4(a) + blockIdx.x;
+    if (!(st & 1u)) {
+        if (w.lane == 0) atomicAdd(&mx->finished, 1u);
+        st |= 1u;
+    }
+    if (!(st & 2u)) {
+        if (w.lane == 0) {
+            const uint32_t t = atomicAdd(&mx->reg_tail, 1u);
+            if (t < kDnRegX)
+                __hip_atomic_store(dn_reg4(a) + (size_t)(blockIdx.x % kDnXcds) * kDnRegX + t,
+                                   ((unsigned long long)epoch << 32) | blockIdx.x, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        st |= 2u;
+    }
+    // relaxed polls: an acquire at agent scope invalidates the XCD's L2, and thousands of idle
+    // waves doing that every few microseconds evict the working waves' stacks and inputs
+    const unsigned long long m = ld_agent64(mbox);
+    const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
+    if (mhi == epoch) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the item's words
+        // delivered: the donor took this wave out of `finished`; its registration is spent
+        const uint32_t idx = __builtin_amdgcn_readfirstlane((uint32_t)m);
+        if (w.lane == 0) __hip_atomic_store(mbox, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (w.lane == 0) s_dnwave4 = 0u;
+        if (w.half == 0) dn_start_item4(w, a, c, 0u, idx, s_slot);
+        A0 = 0x00000000FFFFFFFFull;
+        return 2;
+    }
+    st += 0x100u;                             // polls; the grid-wide idle count every 16th
+    if (w.lane == 0) s_dnwave4 = st;
+    if (((st >> 8) & 15u) == 1u) {
+        uint32_t fin = 0;
+        for (int k = 0; k < kDnXcds; ++k) fin += ld_agent(&ctl->x[k].finished);
+        fin = __builtin_amdgcn_readfirstlane(fin);
+        if (fin >= gridDim.x) {
+            if (w.lane == 0) atomicAdd(&ctl->exit_all, 1u);
+            return 0;
+        }
+    }
+    __builtin_amdgcn_s_sleep(SDK_DN_SLEEP);
+    return 1;
+}
 
 // Locked candidates (pointing and claiming) for the board in slot HI, run at its
 // propagation fixpoints before it branches (SDK_OPT_LOCKED).  Over the 54 box-line
@@ -680,9 +1165,24 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
     statics4<HI>(wr, c);   // the loop lane's LDS addresses: the round's, live anyway
 }
 
-template <int HI>
+template <bool DN, int HI>
 __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c,
                                               int st) {
+    if (DN) {
+        SlotDn* pd = s_dn4 + w.half * 2 + HI;
+        const SlotDn d = *pd;
+        if (d.rec != kDnNone) {       // a part of a donating board: bookkeeping after the step
+            if (w.hl == 0) {
+                const int k = w.half * 2 + HI;
+                s_dnfin4[k] = DnFin{d.rec, d.part, st, b.maxd,
+                                    (unsigned long long)(a.work_rounds == 1 ? (uint64_t)(a.iter - b.rstart) : b.nodes)};
+                atomicOr(&s_dnpend4, 1u << k);
+                *pd = SlotDn{kDnNone, kDnOwner, 0u, 0u};
+            }
+            next_board4<HI>(w, wr, a, b, c);
+            return;
+        }
+    }
     uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
     if (a.count_mode && w.hl == 0 && st != -2 && b.count)
         atomicAdd(a.count, (unsigned long long)b.count);
@@ -759,21 +1259,42 @@ __device__ __forceinline__ void set_cell4(const Lane4& w, Cells4& c, int cell, u
 // DFS level record: every lane keeps the level's branch record -- cell | untried
 // digits << 7, uniform in the half -- in the free upper 16 bits of its own snapshot
 // word y, so a level is one 8-byte word per lane and needs no shared record array.
-template <int HI>
+template <bool DN, int HI>
 __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c, bool bad,
                                            uint2 (*s_stk)[2][64], uint2* g_stk) {
     ++b.nodes;
+    SlotDn dd = SlotDn{kDnNone, kDnOwner, 0u, 0u};
+    if (DN) {
+        dd = s_dn4[w.half * 2 + HI];
+        if (dd.plen & kDnAbort) {     // pruned by dn_check4
+            PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, kDnPruned));
+            return;
+        }
+        // every kDnEvery nodes of a LEX solve: prune / donate check after the step (dn_check4)
+        if ((b.nodes & (kDnEvery - 1u)) == 0u && b.order == ORDER_LEX && !a.count_mode && w.hl == 0)
+            atomicOr(&s_dnpend4, 16u << (w.half * 2 + HI));
+    }
     const uint32_t x0 = fld<HI>(c.x0), x1 = fld<HI>(c.x1), x2 = fld<HI>(c.x2);
     const uint32_t s0 = fld<HI>(c.s0), s1 = fld<HI>(c.s1), s2 = fld<HI>(c.s2);
     int r = bad ? P_CONTRA
                 : (half_any4(w, w.act && (x0 | x1 | x2) != 0u) ? P_OPEN : P_SOLVED);
     if (a.budget && b.nodes > a.budget) {
-        PROF4(3, finish_board4<HI>(w, wr, a, b, c, -2));
+        PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, -2));
         return;
     }
     if (r == P_SOLVED) {
         ++b.count;
-        if (b.count == 1 && w.act && a.out) {
+        if (DN && dd.rec != kDnNone) {
+            // a part of a donating board (exact: every closed cell holds a digit): its own
+            // completion store, the board's answer is chosen when its last part ends
+            if (b.count == 1 && w.act) {
+                const DnRec* r = dn_recs4(a) + dd.rec;
+                uint8_t* dst = const_cast<uint8_t*>(dn_sol4(a, r, dd.part));
+                dst[w.c0] = (uint8_t)__ffs(s0);
+                dst[w.c0 + 27] = (uint8_t)__ffs(s1);
+                dst[w.c0 + 54] = (uint8_t)__ffs(s2);
+            }
+        } else if (b.count == 1 && w.act && a.out) {
             uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
             const uint8_t* sin = w.s_in + HI * 81;
             const uint32_t i0 = sin[w.c0], i1 = sin[w.c0 + 27], i2 = sin[w.c0 + 54];
@@ -791,7 +1312,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
                 b.lim = 1;
                 start_board4<HI>(w, a, b, c, false);
             } else {                                           // found, or the count limit
-                PROF4(3, finish_board4<HI>(w, wr, a, b, c, 1));
+                PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, 1));
             }
             return;
         }
@@ -833,9 +1354,10 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
 #endif
         return;
     }
-    // contradiction: resume the deepest level with untried digits
-    if (b.depth == 0) {
-        PROF4(3, finish_board4<HI>(w, wr, a, b, c, b.count > 0 ? 1 : 0));
+    // contradiction: resume the deepest level with untried digits (a donating part: levels
+    // below its first live one were given away)
+    if (b.depth == (DN ? dd.base : 0u)) {
+        PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, b.count > 0 ? 1 : 0));
         return;
     }
 #if SDK_SOLVE4_PROFILE
@@ -869,14 +1391,14 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
 }
 
 // step of slot HI: its state comes from and returns to LDS; returns whether the slot is active
-template <int HI>
+template <bool DN, int HI>
 __device__ __forceinline__ bool step4(const Lane4& wr, const Args4& a, Cells4& c, bool bad, uint2 (*s_stk)[2][64],
                                       uint2* g_stk_all, Slot4* s_slot, uint2* s_region, uint8_t* s_in) {
     const Lane4 w = lane4_fresh(s_region, s_in);
     uint2* g_stk = g_stk_all + (size_t)blockIdx.x * (kMaxDepth * 2 * 64);
     Slot4* p = s_slot + w.half * 2 + HI;
     Slot4 b;
-    PROF4(1 + HI, b = *p; step4_body<HI>(w, wr, a, b, c, bad, s_stk, g_stk); if (w.hl == 0) *p = b);
+    PROF4(1 + HI, b = *p; step4_body<DN, HI>(w, wr, a, b, c, bad, s_stk, g_stk); if (w.hl == 0) *p = b);
     return (b.active & 1u) != 0u;
 }
 
@@ -895,7 +1417,12 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
 }
 
 #ifdef SDK_DEFINE_SOLVE4_KERNEL   // defined in solve4_launch.hip only
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {
+// DN: subtree donation (see "subtree donation" above); solve4_kernel<false> is the plain kernel
+#ifndef SDK_SOLVE4_DN_WAVES_PER_EU
+#define SDK_SOLVE4_DN_WAVES_PER_EU 6
+#endif
+template <bool DN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOLVE4_DN_WAVES_PER_EU : SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {
     __shared__ uint2 s_region[2 * kRegion4];
     __shared__ uint8_t s_in[2 * 2 * 81];
     __shared__ uint2 s_stk[kLds4Levels > 0 ? kLds4Levels : 1][2][64];   // unused when kLds4Levels = 0
@@ -928,6 +1455,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     a.count_stop = args.count_mode && args.limit && args.limit < 0x80000000ull;
     a.count_lim = a.count_stop ? (uint32_t)args.limit : 0x80000000u;
     a.count = args.count;
+    a.dn = static_cast<DnCtl*>(args.donate);
+    if (DN && threadIdx.x < 4) s_dn4[threadIdx.x] = SlotDn{kDnNone, kDnOwner, 0u, 0u};
+    if (DN && threadIdx.x == 0) {
+        s_dnpend4 = 0u;
+        s_dnwave4 = 0u;
+        s_dnepoch4 = ld_agent(&a.dn->epoch);
+    }
     {   // segments share the first n - n/32 boards (rounded to whole chunks); the rest is the tail
         a.tail_chunk = max(1u, args.chunk / SDK_SOLVE4_TAIL_CHUNK_DIV);
         const uint64_t tail = ((args.n / SDK_SOLVE4_TAIL_DIV + args.chunk - 1) / args.chunk) * args.chunk;
@@ -953,7 +1487,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
 #if SDK_SOLVE4_PROFILE
     const uint64_t tl_ = __builtin_amdgcn_s_memtime();
 #endif
-    while ((A0 | A1) != 0) {
+    for (;;) {
+        if ((A0 | A1) == 0) {
+            if (!DN) break;
+            // every slot idle: take a donated item, or leave once the whole grid is idle
+            const int r = dn_idle4(lane4_fresh(s_region, s_in), a, c, A0, s_slot);
+            if (r == 0) break;
+            if (r == 1) continue;
+        }
         uint32_t badw, chg;
         // every board of the wave exact (an inactive slot is not): the shorter round
         if (a.locked && __builtin_amdgcn_ballot_w64(c.E != kC2) == 0)
@@ -969,14 +1510,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
         if (E0 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E0))
-                r = step4<0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot, s_region, s_in);
+                r = step4<DN, 0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot, s_region, s_in);
             A0 = (A0 & ~E0) | (__builtin_amdgcn_ballot_w64(r) & E0);
         }
         if (E1 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E1))
-                r = step4<1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot, s_region, s_in);
+                r = step4<DN, 1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot, s_region, s_in);
             A1 = (A1 & ~E1) | (__builtin_amdgcn_ballot_w64(r) & E1);
+        }
+        if (DN && (E0 | E1) != 0) {
+            // after the steps: bookkeeping of parts that ended, donation / pruning checks
+            const uint32_t pend = __builtin_amdgcn_readfirstlane(s_dnpend4);
+            if (pend != 0u) {
+                const Lane4 wf = lane4_fresh(s_region, s_in);
+                uint2* g_wg = g_stk + (size_t)blockIdx.x * (kMaxDepth * 2 * 64);
+#pragma nounroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    if (!((pend >> k) & 0x11u)) continue;
+                    if (wf.half == (int)(k >> 1)) {
+                        if ((pend >> k) & 1u) dn_finish_part4(wf, a, s_dnfin4[k]);
+                        if ((pend >> (4 + k)) & 1u) dn_check4(wf, a, c, k, s_slot, g_wg);
+                    }
+                }
+                if (threadIdx.x == 0) s_dnpend4 = 0u;
+            }
         }
     }
 #if SDK_SOLVE4_PROFILE

@@ -8,8 +8,17 @@
 namespace sdk {
 
 hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream) {
-    solve4_kernel<<<grid, 64, 0, stream>>>(a);
+    if (a.donate)
+        solve4_kernel<true><<<grid, 64, 0, stream>>>(a);
+    else
+        solve4_kernel<false><<<grid, 64, 0, stream>>>(a);
     return hipGetLastError();
+}
+
+int solve4_dn_blocks_per_cu() {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, solve4_kernel<true>, 64, 0) != hipSuccess) return -1;
+    return blocks;
 }
 
 }  // namespace sdk

@@ -78,6 +78,7 @@ struct SolveArgs {
     uint64_t in_step;          // outputs stay dense (out[i*81], status[i]); 0/1 = contiguous
     int locked;                // QUAD solver: locked-candidates pass at fixpoints (SDK_OPT_LOCKED)
     uint32_t* heads;           // QUAD solver: kHeads dequeue heads, one per XCD segment (nullable)
+    void* donate;              // QUAD solver, LEX solves: subtree-donation area (solve4_kernel.h, DnCtl first)
 };
 
 // per-XCD dequeue: the first n - n/32 boards are cut into kHeads contiguous segments with a

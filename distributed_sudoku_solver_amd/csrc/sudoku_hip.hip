@@ -27,6 +27,7 @@
 namespace sdk {
 hipError_t launch_solve2(const SolveArgs& a, unsigned grid, hipStream_t stream);
 hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream);
+int solve4_dn_blocks_per_cu();   // resident workgroups per CU of solve4_kernel<true>
 }
 
 namespace {
@@ -60,6 +61,35 @@ struct DevBuf {
 
 }  // namespace
 
+namespace sdk {
+// two-phase solve (launch_solve): list the split phase's budget hits, gather them into a
+// dense batch, scatter their answers back
+__global__ void dn_collect_kernel(const int8_t* status, uint64_t n, uint32_t* hits) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (status[i] == -2) hits[1 + atomicAdd(hits, 1u)] = (uint32_t)i;
+}
+__global__ void dn_gather_kernel(const uint8_t* in, const uint16_t* mask, uint64_t in_first, uint64_t in_step,
+                                 const uint32_t* hits, uint32_t m, uint8_t* out, uint16_t* out_mask) {
+    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
+        const uint64_t j = hits[i];
+        const uint8_t* src = in + (in_first + j * in_step) * 81;
+        if (threadIdx.x < 81) out[(uint64_t)i * 81 + threadIdx.x] = src[threadIdx.x];
+        if (threadIdx.x == 0 && mask) out_mask[i] = mask[j];
+    }
+}
+__global__ void dn_scatter_kernel(const uint32_t* hits, uint32_t m, const uint8_t* sub_out, const int8_t* sub_st,
+                                  const uint64_t* sub_work, bool depth, uint8_t* out, int8_t* status, uint64_t* work) {
+    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
+        const uint64_t j = hits[i];
+        if (threadIdx.x < 81) out[j * 81 + threadIdx.x] = sub_out[(uint64_t)i * 81 + threadIdx.x];
+        if (threadIdx.x == 0) {
+            status[j] = sub_st[i];
+            if (work && sub_work) work[j] = depth ? max(work[j], sub_work[i]) : work[j] + sub_work[i];
+        }
+    }
+}
+}  // namespace sdk
+
 struct sdk_ctx {
     int device = 0;
     int cus = 256;
@@ -80,6 +110,12 @@ struct sdk_ctx {
     // workspaces
     DevBuf stack, counter, heads, in, mask, out, status, work, verdict;
     int xcd_heads = 1;             // QUAD: per-XCD dequeue heads (SDK_OPT_XCD_HEADS)
+    int donate = 1;                // QUAD, LEX solves: subtree donation (SDK_OPT_DONATE)
+    DevBuf dn;                     // donation area (solve4_kernel.h: DnCtl, records, items, mailboxes)
+    DevBuf hits, dn_in, dn_mask, dn_out, dn_st, dn_work;   // the two-phase solve's tail boards
+    uint32_t dn_split_boards = 0;  // boards the last two-phase solve passed to the donation kernel
+    uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
+    int dn_blocks_per_cu = 0;      // resident solve4_kernel<true> workgroups per CU (queried once)
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
     // the device-resident frontier of the last sdk_frontier_build (in fr_a)
     uint64_t fr_size = 0;
@@ -97,6 +133,8 @@ struct sdk_ctx {
 };
 
 namespace {
+
+constexpr uint64_t kDnSplitDefault = 256;   // SDK_OPT_DONATE = 1: split budget (search nodes) of the plain phase
 
 int ensure(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes) return SDK_OK;
@@ -154,10 +192,14 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
     return SDK_OK;
 }
 
-int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
-                 uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
-                 unsigned long long* d_counts = nullptr, uint64_t in_first = 0, uint64_t in_step = 1,
-                 int order = -1, int64_t budget = -1) {
+
+// dn_phase (QUAD, LEX solves with SDK_OPT_DONATE): 0 plain launch; 1 the split phase (plain
+// kernel, split budget); 2 the donation kernel solve4_kernel<true> on the full resident grid
+// (see launch_solve)
+int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
+                      uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
+                      unsigned long long* d_counts, uint64_t in_first, uint64_t in_step, int order, int64_t budget,
+                      int dn_phase) {
     // budget: node budget per board for this launch (-1 = the context's SDK_OPT_NODE_BUDGET)
     const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
     if (n == 0) return SDK_OK;
@@ -239,6 +281,38 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     a.in_step = in_step;
     a.locked = c->locked;
     a.heads = nullptr;
+    a.donate = nullptr;
+    unsigned grid_used = grid;
+    if (four && !count_mode && dn_phase == 2) {
+        // subtree donation: idle waves wait for items while any wave of the grid works, so the
+        // grid is the resident one (its occupancy, not waves_per_cu2), whatever the batch size:
+        // waves without a board of their own are the helpers
+        if (c->dn.bytes < sdk::kDnBytes) {
+            rc = ensure(c->dn, sdk::kDnBytes);
+            if (rc) return rc;
+            HIPCALL(hipMemsetAsync(c->dn.p, 0, sdk::kDnBytes, c->stream));   // entries of epoch 0
+            c->dn_epoch = 0;
+        }
+        if (c->dn_blocks_per_cu <= 0) {
+            c->dn_blocks_per_cu = sdk::solve4_dn_blocks_per_cu();
+            if (c->dn_blocks_per_cu <= 0) return fail(SDK_EHIP, "occupancy query for the donation kernel failed");
+        }
+        if (++c->dn_epoch == 0) {   // 2^32 launches: clear the stale entries once
+            HIPCALL(hipMemsetAsync(c->dn.p, 0, sdk::kDnBytes, c->stream));
+            c->dn_epoch = 1;
+        }
+        HIPCALL(hipMemsetAsync(c->dn.p, 0, sizeof(sdk::DnCtl), c->stream));
+        HIPCALL(hipMemsetD32Async(static_cast<hipDeviceptr_t>(c->dn.p), (int)c->dn_epoch, 1, c->stream));
+        a.donate = c->dn.p;
+        grid_used = (unsigned)std::max<uint64_t>(
+            1, std::min<uint64_t>((uint64_t)c->cus * (uint64_t)std::min(c->dn_blocks_per_cu, c->waves_per_cu2),
+                                  (uint64_t)sdk::kDnMbox));
+        if (grid_used > grid) {
+            rc = ensure(c->stack, (size_t)grid_used * stack_words * sizeof(uint32_t));
+            if (rc) return rc;
+            a.stack = static_cast<uint32_t*>(c->stack.p);
+        }
+    }
     if (four && c->xcd_heads) {
         rc = ensure(c->heads, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t));
         if (rc) return rc;
@@ -249,7 +323,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     rc = timer_begin(c, &stop);
     if (rc) return rc;
     if (four) {
-        HIPCALL(sdk::launch_solve4(a, grid, c->stream));
+        HIPCALL(sdk::launch_solve4(a, grid_used, c->stream));
     } else if (two) {
         HIPCALL(sdk::launch_solve2(a, grid, c->stream));
     } else {
@@ -257,6 +331,63 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     }
     HIPCALL(hipGetLastError());
     if ((rc = timer_end(c, stop))) return rc;
+    return SDK_OK;
+}
+
+// Solve launch.  QUAD LEX solves with SDK_OPT_DONATE run in two phases: every board first
+// in the plain kernel with at most `split` search nodes (the C4/C2 path is that launch
+// alone); the few boards that need more -- the launch's tail -- are gathered and solved
+// again by solve4_kernel<true> on the full resident grid, where idle waves take subtrees
+// of the heavy boards (subtree donation, solve4_kernel.h), and scattered back.  Results
+// are the ones a single slot finds (same boards, statuses; `work` adds both phases).
+int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
+                 uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
+                 unsigned long long* d_counts = nullptr, uint64_t in_first = 0, uint64_t in_step = 1,
+                 int order = -1, int64_t budget = -1) {
+    const int eff_order = order >= 0 ? order : c->order;
+    const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
+    const uint64_t split = c->donate == 1 ? kDnSplitDefault : (uint64_t)c->donate;
+    c->dn_split_boards = 0;
+    const bool two_phase = n > 0 && !count_mode && c->donate && c->solver == SDK_SOLVER_QUAD &&
+                           eff_order == SDK_ORDER_LEX && d_out && d_status && (node_budget == 0 || node_budget > split);
+    if (!two_phase)
+        return launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, count_mode, limit, d_count, d_counts,
+                                 in_first, in_step, order, budget, 0);
+    int rc;
+    if ((rc = ensure(c->hits, (n + 1) * sizeof(uint32_t)))) return rc;
+    HIPCALL(hipMemsetAsync(c->hits.p, 0, sizeof(uint32_t), c->stream));
+    if ((rc = launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, 0, 0, nullptr, nullptr, in_first, in_step,
+                                order, (int64_t)split, 1)))
+        return rc;
+    sdk::dn_collect_kernel<<<(unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->cus * 8), 256, 0, c->stream>>>(
+        d_status, n, static_cast<uint32_t*>(c->hits.p));
+    HIPCALL(hipGetLastError());
+    uint32_t m = 0;
+    HIPCALL(hipMemcpyAsync(&m, c->hits.p, sizeof m, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    c->dn_split_boards = m;
+    if (m == 0) return SDK_OK;
+    if ((rc = ensure(c->dn_in, (size_t)m * 81)) || (rc = ensure(c->dn_out, (size_t)m * 81)) ||
+        (rc = ensure(c->dn_st, m)) || (d_work && (rc = ensure(c->dn_work, (size_t)m * 8))) ||
+        (d_mask && (rc = ensure(c->dn_mask, (size_t)m * 2))))
+        return rc;
+    const uint32_t* hits = static_cast<const uint32_t*>(c->hits.p) + 1;
+    const unsigned g = (unsigned)std::min<uint64_t>(m, (uint64_t)c->cus * 16);
+    sdk::dn_gather_kernel<<<g, 128, 0, c->stream>>>(d_in, d_mask, in_first, in_step, hits, m,
+                                                    static_cast<uint8_t*>(c->dn_in.p),
+                                                    static_cast<uint16_t*>(d_mask ? c->dn_mask.p : nullptr));
+    HIPCALL(hipGetLastError());
+    if ((rc = launch_solve_once(c, static_cast<uint8_t*>(c->dn_in.p),
+                                d_mask ? static_cast<uint16_t*>(c->dn_mask.p) : nullptr,
+                                static_cast<uint8_t*>(c->dn_out.p), static_cast<int8_t*>(c->dn_st.p),
+                                d_work ? static_cast<uint64_t*>(c->dn_work.p) : nullptr, m, 0, 0, nullptr, nullptr, 0,
+                                1, order, (int64_t)node_budget, 2)))
+        return rc;
+    sdk::dn_scatter_kernel<<<g, 128, 0, c->stream>>>(hits, m, static_cast<const uint8_t*>(c->dn_out.p),
+                                                     static_cast<const int8_t*>(c->dn_st.p),
+                                                     d_work ? static_cast<const uint64_t*>(c->dn_work.p) : nullptr,
+                                                     c->work_rounds == SDK_WORK_DEPTH, d_out, d_status, d_work);
+    HIPCALL(hipGetLastError());
     return SDK_OK;
 }
 
@@ -534,7 +665,8 @@ int sdk_destroy(sdk_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf* b : {&c->stack, &c->counter, &c->heads, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
+    for (DevBuf* b : {&c->dn, &c->hits, &c->dn_in, &c->dn_mask, &c->dn_out, &c->dn_st, &c->dn_work,
+                      &c->stack, &c->counter, &c->heads, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
                       &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status,
                       &c->fr_mask, &c->tsum, &c->fr_ctl})
         if (b->p) (void)hipFree(b->p);
@@ -598,6 +730,14 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 0 || value > 2) return fail(SDK_EINVAL, "locked must be 0, 1 or 2");
             c->locked = (int)value;
             return SDK_OK;
+        case SDK_OPT_DONATED:
+            return fail(SDK_EINVAL, "SDK_OPT_DONATED is read-only");
+        case SDK_OPT_SPLIT_BOARDS:
+            return fail(SDK_EINVAL, "SDK_OPT_SPLIT_BOARDS is read-only");
+        case SDK_OPT_DONATE:
+            if (value < 0 || value > (1 << 30)) return fail(SDK_EINVAL, "donate must be 0, 1 or a split budget >= 2");
+            c->donate = (int)value;
+            return SDK_OK;
         case SDK_OPT_XCD_HEADS:
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "xcd heads must be 0 or 1");
             c->xcd_heads = (int)value;
@@ -609,6 +749,18 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
         default:
             return fail(SDK_EINVAL, "unknown option %d", key);
     }
+}
+
+// diagnostics (not in the header): the donation control block of the last donating launch
+extern "C" int sdk_debug_dn_ctl(sdk_ctx* c, uint32_t* out16) {
+    if (!c || !out16) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    std::memset(out16, 0, 64);
+    if (!c->dn.p) return SDK_OK;
+    HIPCALL(hipSetDevice(c->device));
+    HIPCALL(hipMemcpyAsync(out16, c->dn.p, 64, hipMemcpyDeviceToHost, c->stream));   // the global words
+    HIPCALL(hipStreamSynchronize(c->stream));
+    return SDK_OK;
 }
 
 int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
@@ -628,6 +780,19 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_TIMING: *value = c->timing ? 1 : 0; return SDK_OK;
         case SDK_OPT_LOCKED: *value = c->locked; return SDK_OK;
         case SDK_OPT_XCD_HEADS: *value = c->xcd_heads; return SDK_OK;
+        case SDK_OPT_DONATE: *value = c->donate; return SDK_OK;
+        case SDK_OPT_SPLIT_BOARDS: *value = c->dn_split_boards; return SDK_OK;
+        case SDK_OPT_DONATED: {
+            // items handed out by the last donating launch (waits for it on the context's stream)
+            *value = 0;
+            if (!c->dn.p || c->dn_epoch == 0 || c->dn_split_boards == 0) return SDK_OK;
+            HIPCALL(hipSetDevice(c->device));
+            sdk::DnCtl h{};
+            HIPCALL(hipMemcpyAsync(&h, c->dn.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+            HIPCALL(hipStreamSynchronize(c->stream));
+            *value = (int64_t)h.delivered;
+            return SDK_OK;
+        }
         case SDK_OPT_TIMER_EVENTS: *value = (int64_t)c->events.size(); return SDK_OK;
         default: return fail(SDK_EINVAL, "unknown option %d", key);
     }

@@ -81,6 +81,19 @@ extern "C" {
                                  /* every node; same answers, fewer search nodes         */
 #define SDK_OPT_XCD_HEADS    14  /* QUAD solver: 1 = one dequeue head per XCD segment of */
                                  /* the batch (default), 0 = one shared head             */
+#define SDK_OPT_DONATE       15  /* QUAD solver, SDK_ORDER_LEX solves: two-phase solve   */
+                                 /* with subtree donation.  1 (default) or a split       */
+                                 /* budget >= 2: every board first gets at most that     */
+                                 /* many search nodes (1: 256); the boards that need     */
+                                 /* more are solved again by the donation kernel, where  */
+                                 /* idle waves take a heavy board's shallowest untried   */
+                                 /* branches.  Same boards and statuses; `work` adds up  */
+                                 /* both phases and the board's parts.  0 = off: one     */
+                                 /* launch, every board searched by one slot             */
+#define SDK_OPT_DONATED      16  /* read-only: branches handed to idle waves by the last */
+                                 /* solve's donation phase (waits for it)                */
+#define SDK_OPT_SPLIT_BOARDS 17  /* read-only: boards the last solve passed to its       */
+                                 /* donation phase                                       */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

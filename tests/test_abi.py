@@ -42,3 +42,13 @@ def test_error_path_without_gpu_is_clean():
         assert lib.sdk_create(0, ctypes.byref(ctx)) != 0
         assert lib.sdk_last_error()
     assert lib.sdk_set_option(None, 1, 0) == L.SDK_EINVAL
+
+
+def test_header_constants_match_binding():
+    """Every #define SDK_* integer constant of the header has the same value in _lib.py."""
+    text = open(L.HEADER).read()
+    for name, value in re.findall(r"#define\s+(SDK_[A-Z0-9_]+)\s+(-?\d+)u?\b", text):
+        if hasattr(L, name):
+            assert getattr(L, name) == int(value), name
+    for name in ("SDK_OPT_DONATE", "SDK_OPT_DONATED", "SDK_OPT_XCD_HEADS", "SDK_OPT_LOCKED"):
+        assert hasattr(L, name), name

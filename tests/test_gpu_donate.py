@@ -1,0 +1,174 @@
+"""Two-phase solve with subtree donation (SDK_OPT_DONATE, solve4_kernel<true>): boards that
+need more than the split budget are solved again by the donation kernel, where idle waves
+take their shallowest untried branches.  Whatever is donated, every board, status and
+lex-first answer must be the one a single slot finds (and the reference's: the oracle's
+naive DFS, DHT_Node.py:474-538)."""
+import numpy as np
+import pytest
+
+from distributed_sudoku_solver_amd import synth, _lib as L
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_puzzles(n, seed, lo_clues, hi_clues):
+    rng = np.random.default_rng(seed)
+    _, sol = synth.make_17clue(n, seed=seed)
+    keep = rng.random((n, 81)) < rng.uniform(lo_clues, hi_clues, (n, 1)) / 81.0
+    return np.where(keep, sol, 0).astype(np.uint8)
+
+
+def _masks(n, seed):
+    rng = np.random.default_rng(seed)
+    lo = rng.integers(1, 10, n)
+    hi = np.minimum(10, lo + rng.integers(1, 10, n))
+    return np.array([O.range_mask(a, b) for a, b in zip(lo, hi)], dtype=np.uint16)
+
+
+SPLIT = 16    # a small split budget: most searching boards go through the donation phase
+
+
+def _solve(engine, boards, masks=None, donate=SPLIT, budget=None):
+    engine.set_option(L.SDK_OPT_DONATE, donate)
+    try:
+        out, st, work = engine.solve_batch(boards, masks, want_work=True, budget=budget)
+        donated = engine.get_option(L.SDK_OPT_DONATED) if donate else 0
+        split = engine.get_option(L.SDK_OPT_SPLIT_BOARDS)
+    finally:
+        engine.set_option(L.SDK_OPT_DONATE, 1)
+    if not donate:
+        assert split == 0
+    return out, st, work, donated
+
+
+_HARD = {}
+
+
+def _heavy_minimal(engine, n_scan, keep, seed):
+    """The `keep` puzzles of a slice of the committed hard set (distinct minimal unique puzzles
+    that need >= 20 nodes of a singles DFS) that take solve4 the most search nodes."""
+    if "p" not in _HARD:
+        _HARD["p"], _HARD["s"], _ = synth.load_hard(threads=16)
+    lo = seed % (len(_HARD["p"]) - n_scan)
+    p, s = _HARD["p"][lo:lo + n_scan], _HARD["s"][lo:lo + n_scan]
+    _, st, work, _ = _solve(engine, p, donate=0)
+    assert (st == 1).all()
+    idx = np.argsort(-work.astype(np.int64), kind="stable")[:keep]
+    return p[idx], s[idx], work[idx]
+
+
+def test_donation_option_roundtrip(engine):
+    assert engine.get_option(L.SDK_OPT_DONATE) == 1
+    for v in (0, 2, 300):
+        engine.set_option(L.SDK_OPT_DONATE, v)
+        assert engine.get_option(L.SDK_OPT_DONATE) == v
+    engine.set_option(L.SDK_OPT_DONATE, 1)
+    with pytest.raises(L.SudokuHipError):
+        engine.set_option(L.SDK_OPT_DONATE, -1)
+    for ro in (L.SDK_OPT_DONATED, L.SDK_OPT_SPLIT_BOARDS):
+        with pytest.raises(L.SudokuHipError):
+            engine.set_option(ro, 1)
+
+
+def test_easy_batch_takes_one_launch(engine):
+    """Boards within the split budget never reach the donation phase (the C4 launch alone)."""
+    p, s = synth.make_17clue(100_000, seed=9)
+    out, st, _, donated = _solve(engine, p, donate=1)
+    assert engine.get_option(L.SDK_OPT_SPLIT_BOARDS) == 0 and donated == 0
+    assert (st == 1).all() and (out == s).all()
+
+
+def test_heavy_unique_boards_donate_and_match(engine):
+    """A few heavy minimal puzzles alone on the chip: the whole grid is idle, so they donate;
+    every board is still its generating grid, and the summed work covers the single-slot work."""
+    p, s, w0 = _heavy_minimal(engine, 20000, 64, seed=3)
+    assert w0.min() > 4 * SPLIT
+    out, st, work, donated = _solve(engine, p)
+    assert engine.get_option(L.SDK_OPT_SPLIT_BOARDS) == len(p) and donated > 0
+    assert (st == 1).all() and (out == s).all()
+    assert (work >= w0).mean() > 0.5      # both phases and every part are counted
+    out0, st0, _, _ = _solve(engine, p, donate=0)
+    assert (out0 == out).all() and (st0 == st).all()
+
+
+@pytest.mark.parametrize("n", [1, 4, 37, 2000])
+def test_multi_solution_lex_first_with_donation(engine, n):
+    """Sparse boards (many completions) with random first-cell ranges: the donated parts find
+    completions in any order; the answer must still be the lex-first one (oracle)."""
+    puz = _random_puzzles(n, 300 + n, 14, 24)
+    masks = _masks(n, 301 + n)
+    out, st, _, _ = _solve(engine, puz, masks, budget=0)
+    out0, st0, _, _ = _solve(engine, puz, masks, donate=0, budget=0)
+    assert (st == st0).all() and (out == out0).all()
+    ref_out, ref_st, _ = O.naive_solve_batch(puz, masks, budget=20_000_000, threads=16)
+    done = ref_st != -2
+    assert done.mean() > 0.8
+    assert (st[done] == ref_st[done]).all() and (out[done] == ref_out[done]).all()
+
+
+def test_unsolvable_and_budget_hit_with_donation(engine):
+    """'55' + 79 zeros (no completion, propagation cannot refute it) with a node budget: the
+    donated parts hit the budget, so the board is SDK_BUDGET_HIT (undecided), never NO_SOLUTION
+    and never a completion; refutable boards in the same launch stay exact."""
+    c55 = np.zeros((1, 81), np.uint8)
+    c55[0, :2] = 5
+    p, s, _ = _heavy_minimal(engine, 4000, 8, seed=7)
+    dup = s[:4].copy()
+    dup[:, 0] = dup[:, 1]                                          # a given-vs-given conflict
+    boards = np.concatenate([c55, p, np.where(np.arange(81) < 30, dup, 0).astype(np.uint8)])
+    out, st, _, donated = _solve(engine, boards, budget=5000)
+    assert donated > 0
+    assert st[0] == L.SDK_BUDGET_HIT and (out[0] == c55[0]).all()
+    assert (st[1:9] == 1).all() and (out[1:9] == s).all()
+    assert (st[9:] != L.SDK_BUDGET_HIT).all()
+    ref_out, ref_st, _ = O.naive_solve_batch(boards[9:], budget=20_000_000, threads=4)
+    ok = ref_st != -2                         # the naive DFS may run out on a given-vs-given conflict
+    assert (st[9:][ok] == ref_st[ok]).all() and (out[9:][ok] == ref_out[ok]).all()
+    o0, s0, _, _ = _solve(engine, boards[9:], donate=0, budget=5000)
+    assert (s0 == st[9:]).all() and (o0 == out[9:]).all()
+
+
+def _corrupt(p, seed):
+    """Change one clue of each puzzle to a digit its row, column and box do not hold: the units
+    stay exact (no duplicated given) and the board almost always loses every completion, which
+    propagation alone rarely proves -- unsolvable boards that search and donate."""
+    rng = np.random.default_rng(seed)
+    out = p.copy()
+    for b in out:
+        for i in rng.permutation(np.flatnonzero(b)):
+            r, c = divmod(int(i), 9)
+            br, bc = 3 * (r // 3), 3 * (c // 3)
+            used = set(b[9 * r: 9 * r + 9]) | set(b[c::9]) | {b[9 * (br + k) + bc + j] for k in range(3) for j in range(3)}
+            free = [d for d in range(1, 10) if d not in used]
+            if free:
+                b[i] = rng.choice(free)
+                break
+    return out
+
+
+def test_donation_under_small_budget_is_never_wrong(engine):
+    """With a tight per-part budget some boards end undecided; every decided board equals the
+    single-slot unbudgeted answer (a budget hit never turns into a wrong completion), on
+    multi-solution, unique and exact unsolvable boards."""
+    heavy = _heavy_minimal(engine, 8000, 200, 99)[0]
+    puz = np.concatenate([_random_puzzles(500, 77, 16, 26), heavy, _corrupt(heavy, 5)])
+    masks = _masks(len(puz), 78)
+    ref, rst, _, _ = _solve(engine, puz, masks, donate=0, budget=0)
+    for budget in (65, 200, 1000):             # all above SPLIT: the donation phase runs
+        out, st, _, _ = _solve(engine, puz, masks, budget=budget)
+        dec = st != L.SDK_BUDGET_HIT
+        assert dec.mean() > 0.3, budget
+        assert (st[dec] == rst[dec]).all() and (out[dec] == ref[dec]).all(), budget
+        assert (out[~dec] == puz[~dec]).all()
+
+
+def test_large_batch_with_hard_tail(engine):
+    """1M easy boards plus heavy minimal puzzles: the heavy ones are solved by donation at the
+    end of the launch; everything equals its known answer."""
+    p17, s17 = synth.make_17clue(1_000_000, seed=123)
+    ph, sh, _ = _heavy_minimal(engine, 20000, 256, seed=11)
+    boards = np.concatenate([p17, ph])
+    out, st, _, _ = _solve(engine, boards)
+    assert (st == 1).all()
+    assert (out[:len(p17)] == s17).all() and (out[len(p17):] == sh).all()

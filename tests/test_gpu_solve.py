@@ -317,6 +317,7 @@ def test_solvers_take_identical_search_paths(engine):
     boards = np.concatenate([p, sparse])
     res = {}
     engine.set_option(L.SDK_OPT_LOCKED, 0)
+    engine.set_option(L.SDK_OPT_DONATE, 0)       # one slot per board: per-board counters comparable
     try:
         for solver in SOLVERS:
             engine.set_option(L.SDK_OPT_SOLVER, solver)
@@ -325,6 +326,7 @@ def test_solvers_take_identical_search_paths(engine):
                 res[(solver, kind)] = engine.solve_batch(boards, want_work=True)
     finally:
         engine.set_option(L.SDK_OPT_LOCKED, 1)
+        engine.set_option(L.SDK_OPT_DONATE, 1)
         engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
         engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
     for kind in (L.SDK_WORK_NODES, L.SDK_WORK_ROUNDS):
@@ -410,6 +412,7 @@ def test_minimal_unique_puzzles_100k(engine):
     ref_out2, ref_st2, _ = O.naive_solve_batch(boards[20000:], budget=20_000_000, threads=16)
     try:
         engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_DEPTH)
+        engine.set_option(L.SDK_OPT_DONATE, 0)   # donated parts count depth from their own root
         for solver in SOLVERS:
             engine.set_option(L.SDK_OPT_SOLVER, solver)
             engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
@@ -420,6 +423,7 @@ def test_minimal_unique_puzzles_100k(engine):
             assert depth.max() > 10, (solver, int(depth.max()))
     finally:
         engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
+        engine.set_option(L.SDK_OPT_DONATE, 1)
         engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
         engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
 

@@ -78,6 +78,9 @@ def parse_args():
                     help="C2 leg: ~30-clue unique puzzles per GPU (0 = skip)")
     ap.add_argument("--minimal-puzzles", type=int, default=1 << 20,
                     help="distinct minimal-puzzle leg, puzzles per GPU (0 = skip)")
+    ap.add_argument("--hard-leg", type=int, default=1,
+                    help="hard-search leg: the committed hard set (100k distinct puzzles that search) and its "
+                         "1000 heaviest, one launch vs the phased solve with subtree donation (0 = skip)")
     ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
     ap.add_argument("--c5-boards", default="15,14",
                     help="C5 boards: 16/15/14 clues (S1 with clues removed; counts 7,309 / 3,481,026 / 18,204,270); "
@@ -393,6 +396,79 @@ def minimal_leg(eng, d, args, synth, L):
                         f"({int((p > 0).sum(1).mean())} clues on average) x seeded symmetries",
             "value": d.world * n * 3 / el, "unit": "puzzles/s", "avg_kernel_ms": k_s * 1000.0,
             "search": stats, "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
+
+
+def _timed_solves(eng, d, p, s, steps):
+    """Wall time of `steps` solve_batch_dev passes over resident boards (+ 1 warm-up), max over
+    ranks; every board checked against its known answer afterwards."""
+    n = len(p)
+    d_in, d_out, d_st = eng.alloc(n * 81), eng.alloc(n * 81), eng.alloc(n)
+    d_in.upload(p)
+    eng.solve_batch_dev(d_in, d_out, d_st, n)
+    eng.synchronize()
+    d.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.solve_batch_dev(d_in, d_out, d_st, n)
+    eng.synchronize()
+    d.barrier()
+    el = d.max(time.perf_counter() - t0) / steps
+    out = np.empty((n, 81), np.uint8)
+    st = np.empty(n, np.int8)
+    d_out.download(out)
+    d_st.download(st)
+    bad = int(d.sum(int(((out != s).any(axis=1) | (st != 1)).sum())))
+    for b in (d_in, d_out, d_st):
+        b.free()
+    return el, bad
+
+
+def hard_leg(eng, d, args, synth, L):
+    """Puzzles that actually search: the committed hard set
+    (distributed_sudoku_solver_amd/data/hard_minimal.npz: 100k distinct minimal unique puzzles that a
+    singles-propagating lowest-cell DFS needs >= 20 nodes for; rank r > 0 takes a seeded symmetry of
+    each), and its 1000 heaviest -- a batch that is all launch tail.  Each timed one launch per board
+    (SDK_OPT_DONATE 0) and with the phased solve (split phase, then the boards over the split budget
+    with subtree donation: exhaustive MRV count-to-2, LEX re-solve of multi-solution boards)."""
+    p, s, _ = synth.load_hard(threads=cpu_share())
+    hp, hs = synth.make_hard_heaviest(1000, threads=cpu_share())
+    if d.rank:
+        rng = np.random.default_rng([args.seed, d.rank, 5])
+        g, rl = synth.random_symmetries(rng, len(p))
+        p, s = synth.apply_symmetries(p, g, rl), synth.apply_symmetries(s, g, rl)
+        g, rl = synth.random_symmetries(rng, len(hp))
+        hp, hs = synth.apply_symmetries(hp, g, rl), synth.apply_symmetries(hs, g, rl)
+    res, bad = {}, 0
+    for name, (bp, bs) in (("hard_100k", (p, s)), ("heaviest_1000", (hp, hs))):
+        legs = {}
+        for mode, dn in (("one_launch", 0), ("donation", 16 if name == "heaviest_1000" else 1)):
+            eng.set_option(L.SDK_OPT_DONATE, dn)
+            el, b = _timed_solves(eng, d, bp, bs, 5)
+            bad += b
+            legs[mode] = {"value": d.world * len(bp) / el, "unit": "puzzles/s", "ms": el * 1000.0,
+                          "split_budget": dn if dn > 1 else (256 if dn else None),
+                          "split_boards": eng.get_option(L.SDK_OPT_SPLIT_BOARDS),
+                          "lex_boards": eng.get_option(L.SDK_OPT_LEX_BOARDS),
+                          "donated": eng.get_option(L.SDK_OPT_DONATED)}
+        eng.set_option(L.SDK_OPT_DONATE, 1)
+        legs["donation_speedup"] = legs["donation"]["value"] / legs["one_launch"]["value"]
+        res[name] = legs
+    stats = {}
+    eng.set_option(L.SDK_OPT_DONATE, 0)     # per-board work of one slot per board
+    for kind, nm in ((L.SDK_WORK_NODES, "nodes"), (L.SDK_WORK_ROUNDS, "rounds"), (L.SDK_WORK_DEPTH, "depth")):
+        eng.set_option(L.SDK_OPT_WORK_COUNTER, kind)
+        _, _, w = eng.solve_batch(p, want_work=True)
+        stats[nm] = {"mean": float(w.mean()), "p50": float(np.percentile(w, 50)), "p99": float(np.percentile(w, 99)),
+                     "p99.9": float(np.percentile(w, 99.9)), "max": int(w.max())}
+    eng.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
+    eng.set_option(L.SDK_OPT_DONATE, 1)
+    res["workload"] = (f"{len(p)} distinct hard puzzles per GPU ({int((p > 0).sum(1).mean())} clues on average, "
+                       f"committed set) and their 1000 heaviest, resident in HBM")
+    res["search"] = stats
+    res["parity"] = {"mismatched_boards": bad, "checked_boards": d.world * 5 * 2 * (len(p) + len(hp))}
+    if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
+        res["cpu_baseline_c_port"] = cpu_baseline_c(p, min(args.cpu_seconds, 5.0), cpu_share())
+    return res
 
 
 def lane_dfs_leg(eng, args, synth, L):
@@ -732,6 +808,11 @@ def main():
     # ------------------------------------------------ distinct minimal puzzles
     if args.minimal_puzzles > 0:
         leg = side("minimal_puzzles", lambda: minimal_leg(eng, d, args, synth, L))
+        bad_total += leg.get("parity", {}).get("mismatched_boards", 0)
+
+    # ------------------------------------------------ puzzles that search
+    if args.hard_leg:
+        leg = side("hard_search", lambda: hard_leg(eng, d, args, synth, L))
         bad_total += leg.get("parity", {}).get("mismatched_boards", 0)
 
     # ------------------------------------------------------------ C5 leg

@@ -519,6 +519,15 @@ struct Args4 : Args2 {
 // smaller one (then SDK_BUDGET_HIT, as for an undonated board).  Only boards whose units
 // are all exact donate (no duplicated or inert given: every closed cell is a digit).
 //
+// Exhaustive mode (launch order MRV: the two-phase solve's phase 2, see sudoku_hip.hip).
+// The boards are searched with MRV branching for at most two completions -- a unique
+// completion is the lex-first one (the reference's answer).  Every part of a board must
+// then be searched to its end, so every donated subtree is needed work.  The parts add
+// their completions to the record's `total`; at two the board has several completions
+// and every part stops; the finisher writes the unique completion (total 1), restores the
+// input (total 0), or marks the board kDnRetryLex (several completions, or a part that
+// hit the node budget) for a LEX donation launch.
+//
 // Hand-off without a shared queue word: a wave whose four slots are idle counts itself
 // in `finished`, registers its id once (reg[reg_tail++]) and polls only its own mailbox.
 // A donor takes registrations (reg_head += k, at most as many as are registered), takes
@@ -539,9 +548,11 @@ struct DnXcd {
 };
 struct DnCtl {
     uint32_t epoch;           // launch number (host): mailbox and registration entries carry it
+    uint32_t delivered;       // items handed out by the solve's donation launches (host resets it
+                              // per solve; every other word is reset per launch)
     uint32_t item_alloc;      // item records handed out
     uint32_t nrec;            // board records handed out
-    uint32_t delivered, exit_all, parts_ended, finalized;   // diagnostics
+    uint32_t exit_all, parts_ended, finalized;   // diagnostics
     uint32_t pad[25];
     DnXcd x[kDnXcds];
 };
@@ -553,7 +564,7 @@ constexpr uint32_t kDnMbox = 1u << 14;        // workgroups of a donating launch
 constexpr int kDnList = 16;
 constexpr uint32_t kDnNone = 0xFFFFFFFFu, kDnOwner = 0xFFFFFFFEu;
 #ifndef SDK_DN_EVERY
-#define SDK_DN_EVERY 64
+#define SDK_DN_EVERY 16
 #endif
 constexpr uint32_t kDnEvery = SDK_DN_EVERY;   // nodes between a part's donation / pruning checks
 #ifndef SDK_DN_SLEEP
@@ -563,6 +574,7 @@ constexpr uint32_t kDnEvery = SDK_DN_EVERY;   // nodes between a part's donation
 #define SDK_DN_SLEEP 127
 #endif
 constexpr int kDnPruned = 3;                  // part status: stopped above a known completion
+constexpr int kDnRetryLex = 3;                // board status of an exhaustive launch: solve again in LEX
 struct DnItem {
     uint32_t board, rec, plen, pad0;
     uint32_t pad[4];
@@ -571,13 +583,19 @@ struct DnItem {
     uint32_t pad2[10];
 };
 struct DnRec {                // one per donating board
-    uint32_t board, open, nsol, nhit, flags, maxd;
+    uint32_t board, open, nhit, flags, maxd;
+    uint32_t lock;            // LEX: guards `best` (taken by one half-wave at a time, see dn_finish_part4)
+    uint32_t version;         // LEX: seqlock of `best` (odd while it is rewritten)
+    uint32_t have;            // LEX: `best` holds a completion
     unsigned long long work;
-    uint32_t sol[kDnList];    // parts that found a completion (kDnOwner: the board's own slot)
-    uint32_t hit[kDnList];    // parts that hit the node budget
-    uint8_t owner_sol[96];
+    uint32_t first;           // exhaustive: the part that met the board's first completion
+    uint32_t total;           // exhaustive: completions met by all parts
+    uint32_t hit[kDnList];    // parts that hit the node budget (more: flags bit 0, undecided)
+    uint8_t best[96];         // LEX: the smallest completion any part met
+    uint8_t owner_sol[96];    // the board's own slot's completion
+    uint32_t pad[20];
 };
-static_assert(sizeof(DnItem) == 384 && sizeof(DnRec) == 256 && sizeof(DnCtl) == 128 * (1 + kDnXcds), "donation layout");
+static_assert(sizeof(DnItem) == 384 && sizeof(DnRec) == 384 && sizeof(DnCtl) == 128 * (1 + kDnXcds), "donation layout");
 constexpr size_t kDnRecOffset = sizeof(DnCtl);
 constexpr size_t kDnItemOffset = kDnRecOffset + (size_t)kDnRecs * sizeof(DnRec);
 constexpr size_t kDnRegOffset = kDnItemOffset + (size_t)kDnItems * sizeof(DnItem);
@@ -669,23 +687,19 @@ __device__ __forceinline__ void dn_prefix4(const Lane4& w, const Args4& a, uint3
     }
 }
 
-// an item part: is some completion of its board already below its root prefix?
+// an item part: is the smallest completion of its board met so far below its root prefix?
+// (`best` is read under its seqlock: a copy torn by a concurrent rewrite is discarded)
 __device__ __forceinline__ bool dn_pruned4(const Lane4& w, const Args4& a, const SlotDn& d) {
     const DnRec* r = dn_recs4(a) + d.rec;
-    const uint32_t ns = min(ld_agent(&r->nsol), (uint32_t)kDnList);
-    if (ns == 0) return false;
-    uint32_t p0, p1, p2;
+    const uint32_t v0 = ld_agent(&r->version);
+    if ((v0 & 1u) || !ld_agent(&r->have)) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    uint32_t s0, s1, s2, p0, p1, p2;
+    dn_digits4(w, r->best, s0, s1, s2);
     dn_prefix4(w, a, d.part, p0, p1, p2);
-    bool pruned = false;
-    for (uint32_t k = 0; k < ns && !pruned; ++k) {
-        const uint32_t id = ld_agent(&r->sol[k]);
-        if (id == kDnNone) continue;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        uint32_t s0, s1, s2;
-        dn_digits4(w, dn_sol4(a, r, id), s0, s1, s2);
-        pruned = half_less4(w, s0, s1, s2, p0, p1, p2, (int)(d.plen & ~kDnAbort));
-    }
-    return pruned;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (ld_agent(&r->version) != v0) return false;
+    return half_less4(w, s0, s1, s2, p0, p1, p2, (int)(d.plen & ~kDnAbort));
 }
 
 // give the highest untried digits of stack level d.base (the shallowest live one) to idle
@@ -695,15 +709,27 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     DnCtl* ctl = a.dn;
     const SlotDn d = *pd;
     if (b.depth <= d.base) return;
-    // the first XCD (from this workgroup's own) with registered idle waves
+    // the first XCD (from this workgroup's own) with registered idle waves; all sixteen
+    // counters are read at once (one memory round trip, not eight)
+    uint32_t tl[kDnXcds], hd[kDnXcds];
+#pragma unroll
+    for (int k = 0; k < kDnXcds; ++k) {
+        tl[k] = ld_agent(&ctl->x[k].reg_tail);
+        hd[k] = ld_agent(&ctl->x[k].reg_head);
+    }
     uint32_t x = kDnXcds, tail = 0, head = 0;
-    for (uint32_t k = 0; k < (uint32_t)kDnXcds; ++k) {
+    for (uint32_t k = 0; k < (uint32_t)kDnXcds && x == kDnXcds; ++k) {
         const uint32_t xx = (blockIdx.x + k) % kDnXcds;
-        tail = ld_agent(&ctl->x[xx].reg_tail);
-        head = ld_agent(&ctl->x[xx].reg_head);
-        if (tail > head && head < kDnRegX) {
+        uint32_t t = 0, h = 0;
+#pragma unroll
+        for (int q = 0; q < kDnXcds; ++q) {
+            t = (uint32_t)q == xx ? tl[q] : t;
+            h = (uint32_t)q == xx ? hd[q] : h;
+        }
+        if (t > h && h < kDnRegX) {
             x = xx;
-            break;
+            tail = t;
+            head = h;
         }
     }
     if (x == kDnXcds) return;                                     // no idle wave waits
@@ -735,16 +761,23 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
         r = half_first4(w, v);
         if (r >= kDnRecs) return;                                 // the tickets stay unserved
         DnRec* R = recs + r;
+        // exhaustive mode: an owner that already met a completion (written to out) carries it
+        const bool carry = b.count > 0u;
+        if (carry && w.act) {
+            const uint8_t* o = a.out + (uint64_t)b.bidx * 81;
+            R->owner_sol[w.c0] = o[w.c0];
+            R->owner_sol[w.c0 + 27] = o[w.c0 + 27];
+            R->owner_sol[w.c0 + 54] = o[w.c0 + 54];
+        }
         if (w.hl == 0) {
             R->board = b.bidx;
             R->open = 1;
-            R->nsol = R->nhit = R->flags = R->maxd = 0;
+            R->nhit = R->flags = R->maxd = R->lock = R->version = R->have = 0;
             R->work = 0;
+            R->total = b.count;
+            R->first = carry ? kDnOwner : kDnNone;
         }
-        if (w.hl < kDnList) {
-            R->sol[w.hl] = kDnNone;
-            R->hit[w.hl] = kDnNone;
-        }
+        if (w.hl < kDnList) R->hit[w.hl] = kDnNone;
         if (w.hl == 0) pd->rec = r;
     }
     uint32_t i0 = 0;
@@ -800,22 +833,16 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
 __device__ __forceinline__ void dn_finalize4(const Lane4& w, const Args4& a, const DnRec* r) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const uint32_t board = ld_agent(&r->board);
-    const uint32_t nsol = ld_agent(&r->nsol), nhit = ld_agent(&r->nhit), flags = ld_agent(&r->flags);
-    const uint32_t ns = min(nsol, (uint32_t)kDnList), nh = min(nhit, (uint32_t)kDnList);
-    bool have = false;
+    const uint32_t nhit = ld_agent(&r->nhit), flags = ld_agent(&r->flags);
+    const uint32_t nh = min(nhit, (uint32_t)kDnList);
+    const bool exhaustive = a.order != ORDER_LEX;
+    const uint32_t total = ld_agent(&r->total);
+    // LEX: the running minimum; exhaustive: the completion of the part that met the first one
+    const bool have = exhaustive ? total == 1u : ld_agent(&r->have) != 0u;
     uint32_t b0 = 0, b1 = 0, b2 = 0;
-    for (uint32_t k = 0; k < ns; ++k) {
-        uint32_t s0, s1, s2;
-        dn_digits4(w, dn_sol4(a, r, ld_agent(&r->sol[k])), s0, s1, s2);
-        if (!have || half_less4(w, s0, s1, s2, b0, b1, b2, 81)) {
-            b0 = s0;
-            b1 = s1;
-            b2 = s2;
-            have = true;
-        }
-    }
-    bool blocked = flags != 0u;   // a list overflowed: undecided
-    for (uint32_t k = 0; k < nh && !blocked; ++k) {
+    if (have) dn_digits4(w, exhaustive ? dn_sol4(a, r, ld_agent(&r->first)) : r->best, b0, b1, b2);
+    bool blocked = flags != 0u;   // the hit list overflowed: undecided
+    for (uint32_t k = 0; k < (exhaustive ? 0u : nh) && !blocked; ++k) {
         const uint32_t id = ld_agent(&r->hit[k]);
         if (id == kDnOwner) {
             blocked = true;       // the board's own part: its region holds the smallest prefixes
@@ -825,7 +852,8 @@ __device__ __forceinline__ void dn_finalize4(const Lane4& w, const Args4& a, con
             blocked = !have || !half_less4(w, b0, b1, b2, p0, p1, p2, (int)dn_items4(a)[id].plen);
         }
     }
-    const int st = blocked ? -2 : (have ? 1 : 0);
+    int st = blocked ? -2 : (have ? 1 : 0);
+    if (exhaustive) st = (total >= 2u || nhit != 0u || flags != 0u) ? kDnRetryLex : (total == 1u ? 1 : 0);
     uint8_t* dst = a.out + (uint64_t)board * 81;
     if (w.act) {
         if (st == 1) {
@@ -852,13 +880,41 @@ __device__ __forceinline__ void dn_finalize4(const Lane4& w, const Args4& a, con
 __device__ __forceinline__ void dn_finish_part4(const Lane4& w, const Args4& a, const DnFin& f) {
     DnRec* r = dn_recs4(a) + f.rec;
     const int st = f.st;
-    __threadfence();              // this part's completion bytes before its list entry
+    __threadfence();              // this part's completion bytes before what follows
+    if (st == 1 && a.order == ORDER_LEX) {
+        // fold the part's completion into the board's running minimum.  Only this half of the
+        // wave runs here (the caller's loop takes one slot at a time), so the spinning lane
+        // never waits on its own wave; other waves' holders finish without it.
+        if (w.hl == 0)
+            while (atomicExch(&r->lock, 1u) != 0u) __builtin_amdgcn_s_sleep(1);   // test-and-set
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const bool had = ld_agent(&r->have) != 0u;
+        uint32_t s0, s1, s2, b0, b1, b2;
+        dn_digits4(w, dn_sol4(a, r, f.part), s0, s1, s2);
+        dn_digits4(w, r->best, b0, b1, b2);
+        if (!had || half_less4(w, s0, s1, s2, b0, b1, b2, 81)) {
+            DnRec* rw = const_cast<DnRec*>(r);
+            if (w.hl == 0) __hip_atomic_store(&rw->version, ld_agent(&r->version) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence();
+            if (w.act) {
+                rw->best[w.c0] = (uint8_t)s0;
+                rw->best[w.c0 + 27] = (uint8_t)s1;
+                rw->best[w.c0 + 54] = (uint8_t)s2;
+            }
+            __threadfence();
+            if (w.hl == 0) {
+                __hip_atomic_store(&rw->have, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&rw->version, ld_agent(&r->version) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __threadfence();
+        if (w.hl == 0) atomicExch(&r->lock, 0u);
+    }
     if (w.hl == 0) {
-        if (st == 1 || st == -2) {
-            uint32_t* cnt = st == 1 ? &r->nsol : &r->nhit;
-            const uint32_t k = atomicAdd(cnt, 1u);
+        if (st == -2) {
+            const uint32_t k = atomicAdd(&r->nhit, 1u);
             if (k < (uint32_t)kDnList)
-                __hip_atomic_store((st == 1 ? r->sol : r->hit) + k, f.part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(r->hit + k, f.part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
                 atomicOr(&r->flags, 1u);
         }
@@ -900,9 +956,9 @@ __device__ __forceinline__ void dn_start_item4(const Lane4& w, const Args4& a, C
     b.bidx = board;
     b.bend = board + 1u;              // the next dequeue goes to the (drained) shared tail
     b.depth = 0;
-    b.order = ORDER_LEX;
+    b.order = a.order == ORDER_LEX ? ORDER_LEX : ORDER_MRV;
     b.count = 0;
-    b.lim = 1;
+    b.lim = a.order == ORDER_LEX ? 1u : 2u;
     b.rstart = a.iter;
     b.active = 3u;
     b.maxd = 0;
@@ -919,7 +975,13 @@ __device__ __forceinline__ void dn_check4(const Lane4& w, const Args4& a, const 
                                           uint2* g_stk) {
     SlotDn* pd = s_dn4 + k;
     const SlotDn d = *pd;
-    if (d.rec != kDnNone && d.part != kDnOwner) {
+    if (a.order != ORDER_LEX) {
+        // exhaustive mode: every part stops once its board has two completions
+        if (d.rec != kDnNone && ld_agent(&dn_recs4(a)[d.rec].total) >= 2u) {
+            if (w.hl == 0) pd->plen = d.plen | kDnAbort;
+            return;
+        }
+    } else if (d.rec != kDnNone && d.part != kDnOwner) {
         if (dn_pruned4(w, a, d)) {
             if (w.hl == 0) pd->plen = d.plen | kDnAbort;
             return;
@@ -1183,6 +1245,8 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
             return;
         }
     }
+    // an exhaustive donation launch re-solves its undecided boards in LEX (see dn_finalize4)
+    if (DN && a.order != ORDER_LEX && st == -2) st = kDnRetryLex;
     uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
     if (a.count_mode && w.hl == 0 && st != -2 && b.count)
         atomicAdd(a.count, (unsigned long long)b.count);
@@ -1271,7 +1335,8 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
             return;
         }
         // every kDnEvery nodes of a LEX solve: prune / donate check after the step (dn_check4)
-        if ((b.nodes & (kDnEvery - 1u)) == 0u && b.order == ORDER_LEX && !a.count_mode && w.hl == 0)
+        if ((b.nodes & (kDnEvery - 1u)) == 0u && b.order == (a.order == ORDER_LEX ? ORDER_LEX : ORDER_MRV) &&
+            !a.count_mode && w.hl == 0)
             atomicOr(&s_dnpend4, 16u << (w.half * 2 + HI));
     }
     const uint32_t x0 = fld<HI>(c.x0), x1 = fld<HI>(c.x1), x2 = fld<HI>(c.x2);
@@ -1287,13 +1352,28 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
         if (DN && dd.rec != kDnNone) {
             // a part of a donating board (exact: every closed cell holds a digit): its own
             // completion store, the board's answer is chosen when its last part ends
+            DnRec* rr = dn_recs4(a) + dd.rec;
             if (b.count == 1 && w.act) {
-                const DnRec* r = dn_recs4(a) + dd.rec;
-                uint8_t* dst = const_cast<uint8_t*>(dn_sol4(a, r, dd.part));
+                uint8_t* dst = const_cast<uint8_t*>(dn_sol4(a, rr, dd.part));
                 dst[w.c0] = (uint8_t)__ffs(s0);
                 dst[w.c0 + 27] = (uint8_t)__ffs(s1);
                 dst[w.c0 + 54] = (uint8_t)__ffs(s2);
             }
+            if (b.order == ORDER_MRV) {
+                // exhaustive mode: the board's completions are summed over its parts
+                uint32_t old = 0;
+                if (w.hl == 0) {
+                    old = atomicAdd(&rr->total, 1u);
+                    if (old == 0u) __hip_atomic_store(&rr->first, dd.part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                old = half_first4(w, old);
+                if (old == 0u) {
+                    r = P_CONTRA;             // the first: search on for a second one
+                    goto backtrack;
+                }
+            }
+            PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, 1));   // LEX: the region's first
+            return;
         } else if (b.count == 1 && w.act && a.out) {
             uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
             const uint8_t* sin = w.s_in + HI * 81;
@@ -1354,6 +1434,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
 #endif
         return;
     }
+backtrack:
     // contradiction: resume the deepest level with untried digits (a donating part: levels
     // below its first live one were given away)
     if (b.depth == (DN ? dd.base : 0u)) {
@@ -1419,7 +1500,9 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
 #ifdef SDK_DEFINE_SOLVE4_KERNEL   // defined in solve4_launch.hip only
 // DN: subtree donation (see "subtree donation" above); solve4_kernel<false> is the plain kernel
 #ifndef SDK_SOLVE4_DN_WAVES_PER_EU
-#define SDK_SOLVE4_DN_WAVES_PER_EU 6
+// the donation kernel runs only the launch tail (few boards, mostly idle helper waves): 96
+// VGPRs at 5 waves per SIMD keep its round free of scratch reloads (at 6: 48 B/lane spilled)
+#define SDK_SOLVE4_DN_WAVES_PER_EU 5
 #endif
 template <bool DN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOLVE4_DN_WAVES_PER_EU : SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {

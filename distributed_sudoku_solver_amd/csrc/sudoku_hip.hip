@@ -64,9 +64,9 @@ struct DevBuf {
 namespace sdk {
 // two-phase solve (launch_solve): list the split phase's budget hits, gather them into a
 // dense batch, scatter their answers back
-__global__ void dn_collect_kernel(const int8_t* status, uint64_t n, uint32_t* hits) {
+__global__ void dn_collect_kernel(const int8_t* status, uint64_t n, int8_t code, uint32_t* hits) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        if (status[i] == -2) hits[1 + atomicAdd(hits, 1u)] = (uint32_t)i;
+        if (status[i] == code) hits[1 + atomicAdd(hits, 1u)] = (uint32_t)i;
 }
 __global__ void dn_gather_kernel(const uint8_t* in, const uint16_t* mask, uint64_t in_first, uint64_t in_step,
                                  const uint32_t* hits, uint32_t m, uint8_t* out, uint16_t* out_mask) {
@@ -112,8 +112,11 @@ struct sdk_ctx {
     int xcd_heads = 1;             // QUAD: per-XCD dequeue heads (SDK_OPT_XCD_HEADS)
     int donate = 1;                // QUAD, LEX solves: subtree donation (SDK_OPT_DONATE)
     DevBuf dn;                     // donation area (solve4_kernel.h: DnCtl, records, items, mailboxes)
-    DevBuf hits, dn_in, dn_mask, dn_out, dn_st, dn_work;   // the two-phase solve's tail boards
-    uint32_t dn_split_boards = 0;  // boards the last two-phase solve passed to the donation kernel
+    DevBuf hits, dn_in, dn_mask, dn_out, dn_st, dn_work, dn_list;        // the phased solve's tail boards
+    DevBuf dn3_in, dn3_mask, dn3_out, dn3_st, dn3_work, dn3_list;         // ... and its LEX re-solves
+    uint32_t dn_split_boards = 0;  // boards the last phased solve passed to the donation kernel
+    uint32_t dn_lex_boards = 0;    // ... and of those, boards re-solved in LEX order
+    int dn_exhaustive = 1;         // phase 2 in MRV count-to-2 order (SDK_OPT_DONATE_MODE)
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
     int dn_blocks_per_cu = 0;      // resident solve4_kernel<true> workgroups per CU (queried once)
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
@@ -301,12 +304,15 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
             HIPCALL(hipMemsetAsync(c->dn.p, 0, sdk::kDnBytes, c->stream));
             c->dn_epoch = 1;
         }
-        HIPCALL(hipMemsetAsync(c->dn.p, 0, sizeof(sdk::DnCtl), c->stream));
+        // every control word but `delivered` (the solve's total, reset by launch_solve)
+        HIPCALL(hipMemsetAsync(static_cast<char*>(c->dn.p) + 8, 0, sizeof(sdk::DnCtl) - 8, c->stream));
         HIPCALL(hipMemsetD32Async(static_cast<hipDeviceptr_t>(c->dn.p), (int)c->dn_epoch, 1, c->stream));
         a.donate = c->dn.p;
+        // helpers: 16 waves per board beyond 64, up to the resident grid (a few tail boards do
+        // not need thousands of idle waves registering and polling)
         grid_used = (unsigned)std::max<uint64_t>(
-            1, std::min<uint64_t>((uint64_t)c->cus * (uint64_t)std::min(c->dn_blocks_per_cu, c->waves_per_cu2),
-                                  (uint64_t)sdk::kDnMbox));
+            1, std::min<uint64_t>({(uint64_t)c->cus * (uint64_t)std::min(c->dn_blocks_per_cu, c->waves_per_cu2),
+                                   (uint64_t)sdk::kDnMbox, 64ull + 16ull * (uint64_t)n}));
         if (grid_used > grid) {
             rc = ensure(c->stack, (size_t)grid_used * stack_words * sizeof(uint32_t));
             if (rc) return rc;
@@ -334,12 +340,68 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     return SDK_OK;
 }
 
-// Solve launch.  QUAD LEX solves with SDK_OPT_DONATE run in two phases: every board first
-// in the plain kernel with at most `split` search nodes (the C4/C2 path is that launch
-// alone); the few boards that need more -- the launch's tail -- are gathered and solved
-// again by solve4_kernel<true> on the full resident grid, where idle waves take subtrees
-// of the heavy boards (subtree donation, solve4_kernel.h), and scattered back.  Results
-// are the ones a single slot finds (same boards, statuses; `work` adds both phases).
+// Solve launch.  QUAD LEX solves with SDK_OPT_DONATE run in phases: every board first in
+// the plain kernel with at most `split` search nodes (the C4/C2 path is that launch alone);
+// the few boards that need more -- the launch's tail -- are gathered and solved again by
+// solve4_kernel<true> on the full resident grid, where idle waves take subtrees of the
+// heavy boards (subtree donation, solve4_kernel.h), and scattered back.  That second launch
+// is exhaustive: MRV branching, at most two completions per board, every donated subtree
+// needed work; a unique completion is the lex-first one.  The boards it finds several
+// completions for (or cannot decide within the budget) are solved a third time in LEX
+// order with donation.  Results are the ones a single slot finds (same boards and
+// statuses; `work` adds up the phases and parts).
+int dn_list(sdk_ctx* c, const int8_t* d_status, uint64_t n, int8_t code, uint32_t* m) {
+    HIPCALL(hipMemsetAsync(c->hits.p, 0, sizeof(uint32_t), c->stream));
+    sdk::dn_collect_kernel<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)c->cus * 8)),
+                             256, 0, c->stream>>>(d_status, n, code, static_cast<uint32_t*>(c->hits.p));
+    HIPCALL(hipGetLastError());
+    HIPCALL(hipMemcpyAsync(m, c->hits.p, sizeof *m, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    return SDK_OK;
+}
+
+// gather the listed boards of (d_in, d_mask) into buf_in/buf_mask, solve them with the
+// donation kernel (order), scatter the answers into (d_out, d_status, d_work)
+int dn_resolve(sdk_ctx* c, uint32_t m, const uint8_t* d_in, const uint16_t* d_mask, uint64_t in_first,
+               uint64_t in_step, uint8_t* d_out, int8_t* d_status, uint64_t* d_work, int order, int64_t budget,
+               DevBuf& buf_in, DevBuf& buf_mask, DevBuf& buf_out, DevBuf& buf_st, DevBuf& buf_work, DevBuf& list) {
+    int rc;
+    if ((rc = ensure(buf_in, (size_t)m * 81)) || (rc = ensure(buf_out, (size_t)m * 81)) || (rc = ensure(buf_st, m)) ||
+        (d_work && (rc = ensure(buf_work, (size_t)m * 8))) || (d_mask && (rc = ensure(buf_mask, (size_t)m * 2))) ||
+        (rc = ensure(list, ((size_t)m + 1) * sizeof(uint32_t))))
+        return rc;
+    // keep this phase's list: the next phase lists into c->hits again
+    HIPCALL(hipMemcpyAsync(list.p, c->hits.p, ((size_t)m + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    const uint32_t* idx = static_cast<const uint32_t*>(list.p) + 1;
+    const unsigned g = (unsigned)std::min<uint64_t>(m, (uint64_t)c->cus * 16);
+    sdk::dn_gather_kernel<<<g, 128, 0, c->stream>>>(d_in, d_mask, in_first, in_step, idx, m,
+                                                    static_cast<uint8_t*>(buf_in.p),
+                                                    static_cast<uint16_t*>(d_mask ? buf_mask.p : nullptr));
+    HIPCALL(hipGetLastError());
+    if ((rc = launch_solve_once(c, static_cast<uint8_t*>(buf_in.p), d_mask ? static_cast<uint16_t*>(buf_mask.p) : nullptr,
+                                static_cast<uint8_t*>(buf_out.p), static_cast<int8_t*>(buf_st.p),
+                                d_work ? static_cast<uint64_t*>(buf_work.p) : nullptr, m, 0, 0, nullptr, nullptr, 0, 1,
+                                order, budget, 2)))
+        return rc;
+    if (order == SDK_ORDER_MRV_UNIQUE) {
+        // boards with several completions (or undecided): LEX order, donation again
+        uint32_t m3 = 0;
+        if ((rc = dn_list(c, static_cast<int8_t*>(buf_st.p), m, (int8_t)sdk::kDnRetryLex, &m3))) return rc;
+        c->dn_lex_boards = m3;
+        if (m3 && (rc = dn_resolve(c, m3, static_cast<uint8_t*>(buf_in.p), d_mask ? static_cast<uint16_t*>(buf_mask.p) : nullptr,
+                                   0, 1, static_cast<uint8_t*>(buf_out.p), static_cast<int8_t*>(buf_st.p),
+                                   d_work ? static_cast<uint64_t*>(buf_work.p) : nullptr, SDK_ORDER_LEX, budget,
+                                   c->dn3_in, c->dn3_mask, c->dn3_out, c->dn3_st, c->dn3_work, c->dn3_list)))
+            return rc;
+    }
+    sdk::dn_scatter_kernel<<<g, 128, 0, c->stream>>>(idx, m, static_cast<const uint8_t*>(buf_out.p),
+                                                     static_cast<const int8_t*>(buf_st.p),
+                                                     d_work ? static_cast<const uint64_t*>(buf_work.p) : nullptr,
+                                                     c->work_rounds == SDK_WORK_DEPTH, d_out, d_status, d_work);
+    HIPCALL(hipGetLastError());
+    return SDK_OK;
+}
+
 int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
                  uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
                  unsigned long long* d_counts = nullptr, uint64_t in_first = 0, uint64_t in_step = 1,
@@ -348,6 +410,7 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
     const uint64_t split = c->donate == 1 ? kDnSplitDefault : (uint64_t)c->donate;
     c->dn_split_boards = 0;
+    c->dn_lex_boards = 0;
     const bool two_phase = n > 0 && !count_mode && c->donate && c->solver == SDK_SOLVER_QUAD &&
                            eff_order == SDK_ORDER_LEX && d_out && d_status && (node_budget == 0 || node_budget > split);
     if (!two_phase)
@@ -355,40 +418,17 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
                                  in_first, in_step, order, budget, 0);
     int rc;
     if ((rc = ensure(c->hits, (n + 1) * sizeof(uint32_t)))) return rc;
-    HIPCALL(hipMemsetAsync(c->hits.p, 0, sizeof(uint32_t), c->stream));
+    if (c->dn.p) HIPCALL(hipMemsetAsync(static_cast<char*>(c->dn.p) + 4, 0, 4, c->stream));   // `delivered`
     if ((rc = launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, 0, 0, nullptr, nullptr, in_first, in_step,
                                 order, (int64_t)split, 1)))
         return rc;
-    sdk::dn_collect_kernel<<<(unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->cus * 8), 256, 0, c->stream>>>(
-        d_status, n, static_cast<uint32_t*>(c->hits.p));
-    HIPCALL(hipGetLastError());
     uint32_t m = 0;
-    HIPCALL(hipMemcpyAsync(&m, c->hits.p, sizeof m, hipMemcpyDeviceToHost, c->stream));
-    HIPCALL(hipStreamSynchronize(c->stream));
+    if ((rc = dn_list(c, d_status, n, (int8_t)-2, &m))) return rc;
     c->dn_split_boards = m;
     if (m == 0) return SDK_OK;
-    if ((rc = ensure(c->dn_in, (size_t)m * 81)) || (rc = ensure(c->dn_out, (size_t)m * 81)) ||
-        (rc = ensure(c->dn_st, m)) || (d_work && (rc = ensure(c->dn_work, (size_t)m * 8))) ||
-        (d_mask && (rc = ensure(c->dn_mask, (size_t)m * 2))))
-        return rc;
-    const uint32_t* hits = static_cast<const uint32_t*>(c->hits.p) + 1;
-    const unsigned g = (unsigned)std::min<uint64_t>(m, (uint64_t)c->cus * 16);
-    sdk::dn_gather_kernel<<<g, 128, 0, c->stream>>>(d_in, d_mask, in_first, in_step, hits, m,
-                                                    static_cast<uint8_t*>(c->dn_in.p),
-                                                    static_cast<uint16_t*>(d_mask ? c->dn_mask.p : nullptr));
-    HIPCALL(hipGetLastError());
-    if ((rc = launch_solve_once(c, static_cast<uint8_t*>(c->dn_in.p),
-                                d_mask ? static_cast<uint16_t*>(c->dn_mask.p) : nullptr,
-                                static_cast<uint8_t*>(c->dn_out.p), static_cast<int8_t*>(c->dn_st.p),
-                                d_work ? static_cast<uint64_t*>(c->dn_work.p) : nullptr, m, 0, 0, nullptr, nullptr, 0,
-                                1, order, (int64_t)node_budget, 2)))
-        return rc;
-    sdk::dn_scatter_kernel<<<g, 128, 0, c->stream>>>(hits, m, static_cast<const uint8_t*>(c->dn_out.p),
-                                                     static_cast<const int8_t*>(c->dn_st.p),
-                                                     d_work ? static_cast<const uint64_t*>(c->dn_work.p) : nullptr,
-                                                     c->work_rounds == SDK_WORK_DEPTH, d_out, d_status, d_work);
-    HIPCALL(hipGetLastError());
-    return SDK_OK;
+    return dn_resolve(c, m, d_in, d_mask, in_first, in_step, d_out, d_status, d_work,
+                      c->dn_exhaustive ? SDK_ORDER_MRV_UNIQUE : SDK_ORDER_LEX, (int64_t)node_budget, c->dn_in,
+                      c->dn_mask, c->dn_out, c->dn_st, c->dn_work, c->dn_list);
 }
 
 // Deterministic breadth-first frontier of one board, left in c->fr_a.
@@ -665,7 +705,8 @@ int sdk_destroy(sdk_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf* b : {&c->dn, &c->hits, &c->dn_in, &c->dn_mask, &c->dn_out, &c->dn_st, &c->dn_work,
+    for (DevBuf* b : {&c->dn, &c->hits, &c->dn_in, &c->dn_mask, &c->dn_out, &c->dn_st, &c->dn_work, &c->dn_list,
+                      &c->dn3_in, &c->dn3_mask, &c->dn3_out, &c->dn3_st, &c->dn3_work, &c->dn3_list,
                       &c->stack, &c->counter, &c->heads, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
                       &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status,
                       &c->fr_mask, &c->tsum, &c->fr_ctl})
@@ -734,6 +775,12 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             return fail(SDK_EINVAL, "SDK_OPT_DONATED is read-only");
         case SDK_OPT_SPLIT_BOARDS:
             return fail(SDK_EINVAL, "SDK_OPT_SPLIT_BOARDS is read-only");
+        case SDK_OPT_LEX_BOARDS:
+            return fail(SDK_EINVAL, "SDK_OPT_LEX_BOARDS is read-only");
+        case SDK_OPT_DONATE_MODE:
+            if (value != 0 && value != 1) return fail(SDK_EINVAL, "donate mode must be 0 (LEX) or 1 (exhaustive)");
+            c->dn_exhaustive = (int)value;
+            return SDK_OK;
         case SDK_OPT_DONATE:
             if (value < 0 || value > (1 << 30)) return fail(SDK_EINVAL, "donate must be 0, 1 or a split budget >= 2");
             c->donate = (int)value;
@@ -782,6 +829,8 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_XCD_HEADS: *value = c->xcd_heads; return SDK_OK;
         case SDK_OPT_DONATE: *value = c->donate; return SDK_OK;
         case SDK_OPT_SPLIT_BOARDS: *value = c->dn_split_boards; return SDK_OK;
+        case SDK_OPT_DONATE_MODE: *value = c->dn_exhaustive; return SDK_OK;
+        case SDK_OPT_LEX_BOARDS: *value = c->dn_lex_boards; return SDK_OK;
         case SDK_OPT_DONATED: {
             // items handed out by the last donating launch (waits for it on the context's stream)
             *value = 0;
@@ -862,6 +911,20 @@ int sdk_timer_read(sdk_ctx* c, double* total_ms, int64_t* launches) {
     }
     *total_ms = tot;
     *launches = (int64_t)c->events_used;
+    return SDK_OK;
+}
+
+// diagnostics (not in the header): durations of the timed launches since sdk_timer_reset
+extern "C" int sdk_debug_timer_list(sdk_ctx* c, double* ms, int64_t cap, int64_t* n) {
+    if (!c || !ms || !n) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    *n = (int64_t)c->events_used;
+    for (size_t i = 0; i < c->events_used && (int64_t)i < cap; ++i) {
+        float v = 0.f;
+        HIPCALL(hipEventElapsedTime(&v, c->events[i].first, c->events[i].second));
+        ms[i] = v;
+    }
     return SDK_OK;
 }
 

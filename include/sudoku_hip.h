@@ -94,6 +94,12 @@ extern "C" {
                                  /* solve's donation phase (waits for it)                */
 #define SDK_OPT_SPLIT_BOARDS 17  /* read-only: boards the last solve passed to its       */
                                  /* donation phase                                       */
+#define SDK_OPT_DONATE_MODE  18  /* the donation phase's order: 1 (default) exhaustive:  */
+                                 /* MRV, at most two completions per board (a unique one */
+                                 /* is the lex-first), boards with several are solved    */
+                                 /* again in LEX with donation; 0: LEX directly          */
+#define SDK_OPT_LEX_BOARDS   19  /* read-only: boards of the last solve's donation phase */
+                                 /* that needed the LEX re-solve                         */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

@@ -37,7 +37,7 @@ def _run_bench(gpus, extra=(), tmp=None):
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "2", "--warmup", "1",
            "--workload", "solve30", "--batch", "301", "--check-boards", "2000", "--check-steps", "1",
-           "--check-warmup", "1", "--c2-puzzles", "0", "--minimal-puzzles", "0", "--count-leg", "0", "--lane-puzzles", "0",
+           "--check-warmup", "1", "--c2-puzzles", "0", "--minimal-puzzles", "0", "--hard-leg", "0", "--count-leg", "0", "--lane-puzzles", "0",
            "--cpu-seconds", "0",
            "--http-requests", "0", "--pmc-summary", "", "--engine-factory", "doubles:BenchStubEngine", *extra]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)

@@ -29,14 +29,16 @@ def _masks(n, seed):
 SPLIT = 16    # a small split budget: most searching boards go through the donation phase
 
 
-def _solve(engine, boards, masks=None, donate=SPLIT, budget=None):
+def _solve(engine, boards, masks=None, donate=SPLIT, budget=None, mode=1):
     engine.set_option(L.SDK_OPT_DONATE, donate)
+    engine.set_option(L.SDK_OPT_DONATE_MODE, mode)
     try:
         out, st, work = engine.solve_batch(boards, masks, want_work=True, budget=budget)
         donated = engine.get_option(L.SDK_OPT_DONATED) if donate else 0
         split = engine.get_option(L.SDK_OPT_SPLIT_BOARDS)
     finally:
         engine.set_option(L.SDK_OPT_DONATE, 1)
+        engine.set_option(L.SDK_OPT_DONATE_MODE, 1)
     if not donate:
         assert split == 0
     return out, st, work, donated
@@ -66,7 +68,10 @@ def test_donation_option_roundtrip(engine):
     engine.set_option(L.SDK_OPT_DONATE, 1)
     with pytest.raises(L.SudokuHipError):
         engine.set_option(L.SDK_OPT_DONATE, -1)
-    for ro in (L.SDK_OPT_DONATED, L.SDK_OPT_SPLIT_BOARDS):
+    assert engine.get_option(L.SDK_OPT_DONATE_MODE) == 1
+    with pytest.raises(L.SudokuHipError):
+        engine.set_option(L.SDK_OPT_DONATE_MODE, 2)
+    for ro in (L.SDK_OPT_DONATED, L.SDK_OPT_SPLIT_BOARDS, L.SDK_OPT_LEX_BOARDS):
         with pytest.raises(L.SudokuHipError):
             engine.set_option(ro, 1)
 
@@ -79,26 +84,34 @@ def test_easy_batch_takes_one_launch(engine):
     assert (st == 1).all() and (out == s).all()
 
 
-def test_heavy_unique_boards_donate_and_match(engine):
+MODES = pytest.mark.parametrize("mode", [1, 0], ids=["exhaustive", "lex"])
+
+
+@MODES
+def test_heavy_unique_boards_donate_and_match(engine, mode):
     """A few heavy minimal puzzles alone on the chip: the whole grid is idle, so they donate;
     every board is still its generating grid, and the summed work covers the single-slot work."""
     p, s, w0 = _heavy_minimal(engine, 20000, 64, seed=3)
     assert w0.min() > 4 * SPLIT
-    out, st, work, donated = _solve(engine, p)
+    out, st, work, donated = _solve(engine, p, mode=mode)
     assert engine.get_option(L.SDK_OPT_SPLIT_BOARDS) == len(p) and donated > 0
     assert (st == 1).all() and (out == s).all()
-    assert (work >= w0).mean() > 0.5      # both phases and every part are counted
+    if mode == 0:
+        assert (work >= w0).mean() > 0.5  # LEX: both phases and every part are counted
     out0, st0, _, _ = _solve(engine, p, donate=0)
     assert (out0 == out).all() and (st0 == st).all()
 
 
+@MODES
 @pytest.mark.parametrize("n", [1, 4, 37, 2000])
-def test_multi_solution_lex_first_with_donation(engine, n):
+def test_multi_solution_lex_first_with_donation(engine, n, mode):
     """Sparse boards (many completions) with random first-cell ranges: the donated parts find
     completions in any order; the answer must still be the lex-first one (oracle)."""
     puz = _random_puzzles(n, 300 + n, 14, 24)
     masks = _masks(n, 301 + n)
-    out, st, _, _ = _solve(engine, puz, masks, budget=0)
+    out, st, _, _ = _solve(engine, puz, masks, budget=0, mode=mode)
+    if mode == 1 and n >= 37:
+        assert engine.get_option(L.SDK_OPT_LEX_BOARDS) > 0     # several completions: the LEX re-solve ran
     out0, st0, _, _ = _solve(engine, puz, masks, donate=0, budget=0)
     assert (st == st0).all() and (out == out0).all()
     ref_out, ref_st, _ = O.naive_solve_batch(puz, masks, budget=20_000_000, threads=16)
@@ -107,7 +120,8 @@ def test_multi_solution_lex_first_with_donation(engine, n):
     assert (st[done] == ref_st[done]).all() and (out[done] == ref_out[done]).all()
 
 
-def test_unsolvable_and_budget_hit_with_donation(engine):
+@MODES
+def test_unsolvable_and_budget_hit_with_donation(engine, mode):
     """'55' + 79 zeros (no completion, propagation cannot refute it) with a node budget: the
     donated parts hit the budget, so the board is SDK_BUDGET_HIT (undecided), never NO_SOLUTION
     and never a completion; refutable boards in the same launch stay exact."""
@@ -117,7 +131,7 @@ def test_unsolvable_and_budget_hit_with_donation(engine):
     dup = s[:4].copy()
     dup[:, 0] = dup[:, 1]                                          # a given-vs-given conflict
     boards = np.concatenate([c55, p, np.where(np.arange(81) < 30, dup, 0).astype(np.uint8)])
-    out, st, _, donated = _solve(engine, boards, budget=5000)
+    out, st, _, donated = _solve(engine, boards, budget=5000, mode=mode)
     assert donated > 0
     assert st[0] == L.SDK_BUDGET_HIT and (out[0] == c55[0]).all()
     assert (st[1:9] == 1).all() and (out[1:9] == s).all()
@@ -147,7 +161,8 @@ def _corrupt(p, seed):
     return out
 
 
-def test_donation_under_small_budget_is_never_wrong(engine):
+@MODES
+def test_donation_under_small_budget_is_never_wrong(engine, mode):
     """With a tight per-part budget some boards end undecided; every decided board equals the
     single-slot unbudgeted answer (a budget hit never turns into a wrong completion), on
     multi-solution, unique and exact unsolvable boards."""
@@ -156,19 +171,20 @@ def test_donation_under_small_budget_is_never_wrong(engine):
     masks = _masks(len(puz), 78)
     ref, rst, _, _ = _solve(engine, puz, masks, donate=0, budget=0)
     for budget in (65, 200, 1000):             # all above SPLIT: the donation phase runs
-        out, st, _, _ = _solve(engine, puz, masks, budget=budget)
+        out, st, _, _ = _solve(engine, puz, masks, budget=budget, mode=mode)
         dec = st != L.SDK_BUDGET_HIT
         assert dec.mean() > 0.3, budget
         assert (st[dec] == rst[dec]).all() and (out[dec] == ref[dec]).all(), budget
         assert (out[~dec] == puz[~dec]).all()
 
 
-def test_large_batch_with_hard_tail(engine):
+@MODES
+def test_large_batch_with_hard_tail(engine, mode):
     """1M easy boards plus heavy minimal puzzles: the heavy ones are solved by donation at the
     end of the launch; everything equals its known answer."""
     p17, s17 = synth.make_17clue(1_000_000, seed=123)
     ph, sh, _ = _heavy_minimal(engine, 20000, 256, seed=11)
     boards = np.concatenate([p17, ph])
-    out, st, _, _ = _solve(engine, boards)
+    out, st, _, _ = _solve(engine, boards, mode=mode)
     assert (st == 1).all()
     assert (out[:len(p17)] == s17).all() and (out[len(p17):] == sh).all()

@@ -7,7 +7,7 @@
 # usage: tools/pmc_c4.sh <outdir>     then: python3 tools/pmc_c4_summary.py <outdir>
 set -o pipefail
 out=$1; root=$(pwd); mkdir -p "$out"; export TMPDIR=/tmp
-OFF="--c2-puzzles 0 --minimal-puzzles 0 --count-leg 0 --lane-puzzles 0 --cpu-seconds 0 --http-requests 0 --pmc-summary="
+OFF="--c2-puzzles 0 --minimal-puzzles 0 --hard-leg 0 --count-leg 0 --lane-puzzles 0 --cpu-seconds 0 --http-requests 0 --pmc-summary="
 C4="$root/bench.py --steps 2 --warmup 1 --check-boards 0 $OFF"
 C3="$root/bench.py --steps 1 --warmup 0 --batch 1024 --check-boards 100000000 --check-steps 2 --check-warmup 1 $OFF"
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"

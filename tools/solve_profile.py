@@ -26,12 +26,15 @@ ap.add_argument("--chunk", type=int, default=0, help="SDK_OPT_SOLVE_CHUNK (0: au
 ap.add_argument("--order", default="lex", choices=["mrv_unique", "lex"])
 ap.add_argument("--locked", type=int, default=1, help="QUAD: locked-candidates pass (SDK_OPT_LOCKED: 0 off, 1 root, 2 all nodes)")
 ap.add_argument("--donate", type=int, default=-1, help="QUAD: SDK_OPT_DONATE (default: library default)")
+ap.add_argument("--donate-mode", type=int, default=-1, help="QUAD: SDK_OPT_DONATE_MODE (1 exhaustive, 0 LEX)")
 args = ap.parse_args()
 
 if args.workload == "minimal":
     p, s = synth.make_minimal_sym(args.n, threads=16)
 elif args.workload == "hard":
     p, s = synth.make_hard_sym(args.n, threads=16)
+elif args.workload == "heavy":
+    p, s = synth.make_hard_heaviest(args.n, threads=16)
 else:
     gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
     p, s = gen(args.n, seed=11)
@@ -49,6 +52,8 @@ with SudokuEngine(0) as eng:
         eng.set_option(L.SDK_OPT_XCD_HEADS, args.xcd_heads)
     if args.donate >= 0:
         eng.set_option(L.SDK_OPT_DONATE, args.donate)
+    if args.donate_mode >= 0:
+        eng.set_option(L.SDK_OPT_DONATE_MODE, args.donate_mode)
     if args.waves_per_cu:
         eng.set_option(wopt, args.waves_per_cu)
     d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)
@@ -62,8 +67,9 @@ with SudokuEngine(0) as eng:
     ms, nl = eng.timer_read()
     out = np.empty((args.n, 81), np.uint8)
     d_out.download(out)
-    print(f"{args.solver} {args.order} lc={args.locked} xh={args.xcd_heads} dn={args.donate} chunk={args.chunk} {args.workload} n={args.n} kernel={ms / nl:.3f} ms  rate={args.n / (ms / nl) * 1e3 / 1e6:.1f} M/s "
-          f"ok={(out == s).all()}", flush=True)
+    per = ms / args.reps       # one solve: one launch, or both launches of a two-phase solve
+    print(f"{args.solver} {args.order} lc={args.locked} xh={args.xcd_heads} dn={args.donate}/{args.donate_mode} chunk={args.chunk} {args.workload} n={args.n} solve={per:.3f} ms "
+          f"({nl // args.reps} launches) rate={args.n / per * 1e3 / 1e6:.1f} M/s ok={(out == s).all()}", flush=True)
     if args.sweep:
         for wpc in (8, 12, 16, 20, 24, 32):
             eng.set_option(wopt, wpc)

@@ -99,6 +99,25 @@ __device__ __forceinline__ void prof4_add(int k, uint64_t v) {
         __VA_ARGS__;  \
     } while (0)
 #endif
+// Timeline build only (tools/build_variant.sh tl -DSDK_SOLVE4_TIMELINE=1, tools/timeline.py):
+// per workgroup, s_memrealtime (100 MHz, one clock for the whole chip) at kernel entry, once
+// both slots of both halves hold their first board, at the last dequeue that returned boards,
+// and at exit -- the launch's dispatch ramp, start-up and drain.
+#ifndef SDK_SOLVE4_TIMELINE
+#define SDK_SOLVE4_TIMELINE 0
+#endif
+#if SDK_SOLVE4_TIMELINE
+constexpr int kTl4Max = 16384;
+__device__ unsigned long long g_tl4[kTl4Max][4];
+#define TL4(k)                                                                   \
+    do {                                                                         \
+        if (blockIdx.x < (unsigned)kTl4Max) g_tl4[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define TL4(k) \
+    do {       \
+    } while (0)
+#endif
 constexpr int kStack4WordsPerBlock = kMaxDepth * 2 * 64 * 2;
 constexpr uint32_t kC2 = 0x01FF01FFu;                 // candidate bits of both boards
 constexpr uint32_t kInert4 = 0x200u;                  // inert marker (one board)
@@ -1200,6 +1219,9 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
             b.bidx = min(base, (uint32_t)a.n);
             b.bend = min(base + (drained ? a.tail_chunk : a.chunk), end);
             b.active = drained ? 2u : 0u;
+#if SDK_SOLVE4_TIMELINE
+            if (w.hl == 0 && b.bidx < b.bend) TL4(2);
+#endif
         } else {
             uint32_t base = 0;
             if (w.hl == 0) base = atomicAdd(a.next, a.chunk);
@@ -1559,8 +1581,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     c.s0 = c.s1 = c.s2 = kInert4x2;
     c.D = kC2;
     c.E = 0;
+    if (threadIdx.x == 0) TL4(0);
     const bool act0 = first_board4<0>(w, a, c, s_slot);
     const bool act1 = first_board4<1>(w, a, c, s_slot);
+    if (threadIdx.x == 0) TL4(1);
 
     // Event detection in scalar registers: one ballot per (flag, slot), each spread
     // to the 32 lanes of the half it came from; a slot's board takes its search step
@@ -1626,6 +1650,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     __syncthreads();
     if (threadIdx.x < 10) atomicAdd(&g_prof4[threadIdx.x], s_prof4[threadIdx.x]);
 #endif
+    if (threadIdx.x == 0) TL4(3);
 }
 #endif  // SDK_DEFINE_SOLVE4_KERNEL
 

@@ -34,3 +34,15 @@ extern "C" int sdk_debug_prof4(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
+
+#if SDK_SOLVE4_TIMELINE
+// timeline build only: the per-workgroup stamps of the last launch (see solve4_kernel.h), zeroed after
+extern "C" int sdk_debug_tl4(unsigned long long* out, int n) {
+    if (n > sdk::kTl4Max) n = sdk::kTl4Max;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sdk::g_tl4), (size_t)n * 4 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    static unsigned long long zero[sdk::kTl4Max][4];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sdk::g_tl4), zero, sizeof(zero)) != hipSuccess) return -1;
+    return 0;
+}
+#endif

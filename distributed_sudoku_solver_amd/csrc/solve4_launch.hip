@@ -4,6 +4,7 @@
 #define SDK_NO_SOLVE_KERNEL
 #define SDK_DEFINE_SOLVE4_KERNEL
 #include "solve4_kernel.h"
+#include "expand4_kernel.h"
 
 namespace sdk {
 
@@ -12,6 +13,11 @@ hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream) 
         solve4_kernel<true><<<grid, 64, 0, stream>>>(a);
     else
         solve4_kernel<false><<<grid, 64, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_expand4(const ExpandArgs& a, unsigned grid, hipStream_t stream) {
+    expand4_kernel<<<grid, 64, 0, stream>>>(a);
     return hipGetLastError();
 }
 

@@ -28,6 +28,7 @@ namespace sdk {
 hipError_t launch_solve2(const SolveArgs& a, unsigned grid, hipStream_t stream);
 hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream);
 int solve4_dn_blocks_per_cu();   // resident workgroups per CU of solve4_kernel<true>
+hipError_t launch_expand4(const ExpandArgs& a, unsigned grid, hipStream_t stream);   // expand4_kernel.h
 }
 
 namespace {
@@ -475,6 +476,9 @@ int run_frontier_levels(sdk_ctx* c, uint64_t m0, bool use_mask, int mode, uint64
     void* buf[2] = {c->fr_a.p, c->fr_b.p};
     const unsigned eg = (unsigned)std::max<uint64_t>(
         1, std::min<uint64_t>((m_exp + sdk::kChunk - 1) / sdk::kChunk, (uint64_t)c->cus * c->waves_per_cu));
+    const bool quad = c->solver == SDK_SOLVER_QUAD;
+    const unsigned eg4 = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>((m_exp + 3) / 4, (uint64_t)c->cus * c->waves_per_cu2));
     const unsigned sg = (unsigned)std::min<uint64_t>(tiles, (uint64_t)c->cus * 4);
     const unsigned gg = (unsigned)std::min<uint64_t>(m_exp, (uint64_t)c->cus * 32);
     hipEvent_t stop;
@@ -493,7 +497,10 @@ int run_frontier_levels(sdk_ctx* c, uint64_t m0, bool use_mask, int mode, uint64
         ea.order = first ? sdk::ORDER_LEX : sdk::ORDER_MRV;
         ea.mask = (level == 0 && use_mask) ? static_cast<const uint16_t*>(c->fr_mask.p) : nullptr;
         ea.keep_leaves = first ? 1 : 0;
-        sdk::expand_kernel<<<eg, 64, 0, c->stream>>>(ea);
+        if (quad)   // four boards per wave (expand4_kernel.h): the same frontier, byte for byte
+            HIPCALL(sdk::launch_expand4(ea, eg4, c->stream));
+        else
+            sdk::expand_kernel<<<eg, 64, 0, c->stream>>>(ea);
         sdk::scan_tiles_kernel<<<sg, 1024, 0, c->stream>>>(static_cast<uint32_t*>(c->nchild.p),
                                                            static_cast<uint64_t*>(c->offs.p), ctl,
                                                            static_cast<uint64_t*>(c->tsum.p));

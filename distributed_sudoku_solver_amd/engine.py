@@ -211,11 +211,21 @@ class SudokuEngine:
         L.check(fn(self.ctx, _ptr(boards), _ptr(verdict), n), "sdk_check_batch_i64" if wide else "sdk_check_batch")
         return verdict
 
-    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         """uint8[n,81] (+ optional uint16[n] first-cell masks) -> (out uint8[n,81], status int8[n], work).
 
         budget: search nodes per board for this call (sdk_solve_batch_budget; 0 = unlimited),
-        None = the context's SDK_OPT_NODE_BUDGET.  A board that runs out is SDK_BUDGET_HIT."""
+        None = the context's SDK_OPT_NODE_BUDGET.  A board that runs out is SDK_BUDGET_HIT.
+        donate: SDK_OPT_DONATE for this call only (0 = one launch, one slot per board: what a
+        bounded slice of search.LexSearch or a node's batch wants), None = the context's."""
+        if donate is not None:
+            old = self.get_option(L.SDK_OPT_DONATE)
+            if int(donate) != old:
+                self.set_option(L.SDK_OPT_DONATE, int(donate))
+                try:
+                    return self.solve_batch(boards, masks, want_work, budget)
+                finally:
+                    self.set_option(L.SDK_OPT_DONATE, old)
         boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
         n = boards.shape[0]
         if masks is not None:

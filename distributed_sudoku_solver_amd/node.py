@@ -548,7 +548,8 @@ class SudokuNode:
         self._split_for_neighbor(batch)
         boards = np.stack([encode_solve_grid(t["sudoku"]) for t in batch])
         masks = np.array([range_to_mask(t.get("range", range(1, 10))) for t in batch], dtype=np.uint16)
-        out, status, work = self.engine.solve_batch(boards, masks, want_work=True, budget=self.node_budget)
+        # one bounded launch: budget hits continue in search.LexSearch slices between batches
+        out, status, work = self.engine.solve_batch(boards, masks, want_work=True, budget=self.node_budget, donate=0)
         self._spent(int(np.asarray(work).sum()))
         for t, b, m, o, st in zip(batch, boards, masks, out, status):
             if st == L.SDK_BUDGET_HIT:

@@ -60,7 +60,7 @@ def default_budget(engine):
 class LexSearch:
     """The reference's answer for one board, found in bounded slices.
 
-    engine   anything with solve_batch(boards, masks, want_work, budget) and
+    engine   anything with solve_batch(boards, masks, want_work, budget, donate) and
              expand(boards, masks, target) -- SudokuEngine on the GPU
     board    uint8[81] (0 empty, 1..9 given, 10..255 inert given)
     mask     first-cell digit mask (the TASK `range`, engine.range_to_mask), None = all
@@ -157,7 +157,8 @@ class LexSearch:
             return True
         boards, masks = self._take(self.width)
         t0 = time.monotonic()
-        out, st, work = self.engine.solve_batch(boards, masks, want_work=True, budget=self.budget)
+        # one bounded launch (no phased solve: this search is the continuation of heavy boards)
+        out, st, work = self.engine.solve_batch(boards, masks, want_work=True, budget=self.budget, donate=0)
         elapsed = time.monotonic() - t0
         self.launches += 1
         if work is not None:
@@ -205,7 +206,7 @@ def solve_bounded(engine, boards, masks=None, budget=DEFAULT_BUDGET, time_limit=
     LexSearch per board that hit it, each until done or `time_limit` seconds (None = no limit).
     Returns (out, status, work) like solve_batch; status SDK_BUDGET_HIT = search exhausted."""
     boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
-    out, st, work = engine.solve_batch(boards, masks, want_work=True, budget=budget)
+    out, st, work = engine.solve_batch(boards, masks, want_work=True, budget=budget, donate=0)
     out, st = np.array(out), np.array(st)
     work = np.zeros(len(boards), np.uint64) if work is None else np.array(work, dtype=np.uint64)
     for i in np.flatnonzero(st == L.SDK_BUDGET_HIT):

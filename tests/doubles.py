@@ -63,7 +63,7 @@ class OracleEngine:
         self.O = O
         self.calls = []
 
-    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         self.calls.append(len(boards))
         out, st, val = self.O.naive_solve_batch(boards, masks, budget=validation_budget(budget, 50_000_000),
                                                 threads=2)

@@ -52,9 +52,9 @@ class _Counting:
     def __init__(self, eng):
         self.eng, self.sizes = eng, []
 
-    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         self.sizes.append(len(boards))
-        return self.eng.solve_batch(boards, masks, want_work, budget)
+        return self.eng.solve_batch(boards, masks, want_work, budget, donate)
 
     def expand(self, boards, masks=None, target=64):
         return self.eng.expand(boards, masks, target)

@@ -23,7 +23,7 @@ class OracleEngine:
         self.batches = []
         self.expansions = 0
 
-    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         self.batches.append(len(boards))
         out, st, val = self.O.naive_solve_batch(boards, masks, budget=validation_budget(budget, 100_000_000),
                                                 threads=2)
@@ -212,7 +212,7 @@ class _FlakyEngine(OracleEngine):
         super().__init__()
         self.fail_next = True
 
-    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         if self.fail_next:
             self.fail_next = False
             raise RuntimeError("simulated launch failure")
@@ -400,7 +400,7 @@ def test_main_mixin_on_stub_matches_golden(solve_cases):
 
 
 class _SlowEngine(OracleEngine):
-    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         time.sleep(0.5)
         return super().solve_batch(boards, masks, want_work, budget)
 
@@ -455,7 +455,7 @@ CONFLICT55 = "55" + "0" * 79          # unsolvable, propagation ca
 class _TinyBudget(OracleEngine):
     """A node budget of b allows only 50 b naive validations: every real search hits it."""
 
-    def solve_batch(self, boards, masks=None, want_work=False, budget=None):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         self.batches.append(len(boards))
         v = 100_000_000 if budget is None else (0 if budget == 0 else 50 * int(budget))
         return self.O.naive_solve_batch(boards, masks, budget=v, threads=2)

@@ -567,12 +567,13 @@ struct DnXcd {
 };
 struct DnCtl {
     uint32_t epoch;           // launch number (host): mailbox and registration entries carry it
-    uint32_t delivered;       // items handed out by the solve's donation launches (host resets it
-                              // per solve; every other word is reset per launch)
+    uint32_t delivered;       // items handed out by the launch
+
     uint32_t item_alloc;      // item records handed out
     uint32_t nrec;            // board records handed out
     uint32_t exit_all, parts_ended, finalized;   // diagnostics
-    uint32_t pad[25];
+    uint32_t next;            // the launch's board dequeue counter
+    uint32_t pad[24];
     DnXcd x[kDnXcds];
 };
 constexpr uint32_t kDnItems = 1u << 16;
@@ -650,6 +651,7 @@ static __shared__ DnFin s_dnfin4[4];
 static __shared__ uint32_t s_dnpend4; // bit k: s_dnfin4[k] waits; bit 4 + k: slot k's check is due
 static __shared__ uint32_t s_dnwave4; // bit 0: counted in `finished`, bit 1: registered, bits 8..: polls
 static __shared__ uint32_t s_dnepoch4;
+static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
 
 // runtime-slot field access (the donation paths run once per loop iteration for any slot)
 __device__ __forceinline__ uint32_t fld_rt(uint32_t w, uint32_t hi) {
@@ -1052,7 +1054,7 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
         uint32_t fin = 0;
         for (int k = 0; k < kDnXcds; ++k) fin += ld_agent(&ctl->x[k].finished);
         fin = __builtin_amdgcn_readfirstlane(fin);
-        if (fin >= gridDim.x) {
+        if (fin >= __builtin_amdgcn_readfirstlane(s_dngrid4)) {
             if (w.lane == 0) atomicAdd(&ctl->exit_all, 1u);
             return 0;
         }
@@ -1528,6 +1530,17 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
 #endif
 template <bool DN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOLVE4_DN_WAVES_PER_EU : SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {
+    // the donation phases are enqueued without the host: their board count comes from the
+    // device (the list the previous phase left), and the launch is the full resident grid, of
+    // which 64 + 16 waves per board take part (a few tail boards do not need thousands of
+    // idle waves registering and polling; none when nothing was listed)
+    uint64_t n = args.n;
+    uint32_t grid = gridDim.x;
+    if constexpr (DN) {
+        if (args.n_dev) n = min<uint64_t>(*args.n_dev, args.n);
+        grid = (uint32_t)min<uint64_t>(gridDim.x, 64ull + 16ull * n);
+        if (n == 0 || blockIdx.x >= grid) return;
+    }
     __shared__ uint2 s_region[2 * kRegion4];
     __shared__ uint8_t s_in[2 * 2 * 81];
     __shared__ uint2 s_stk[kLds4Levels > 0 ? kLds4Levels : 1][2][64];   // unused when kLds4Levels = 0
@@ -1546,7 +1559,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     a.mask = args.mask;
     a.next = args.next;
     a.chunk = args.chunk;
-    a.n = args.n;
+    a.n = n;
     a.order = args.order;
     a.out = args.out;
     a.status = args.status;
@@ -1566,13 +1579,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         s_dnpend4 = 0u;
         s_dnwave4 = 0u;
         s_dnepoch4 = ld_agent(&a.dn->epoch);
+        s_dngrid4 = grid;
     }
     {   // segments share the first n - n/32 boards (rounded to whole chunks); the rest is the tail
         a.tail_chunk = max(1u, args.chunk / SDK_SOLVE4_TAIL_CHUNK_DIV);
-        const uint64_t tail = ((args.n / SDK_SOLVE4_TAIL_DIV + args.chunk - 1) / args.chunk) * args.chunk;
-        a.tail0 = (uint32_t)(args.n - min<uint64_t>(tail, args.n));
+        const uint64_t tail = ((n / SDK_SOLVE4_TAIL_DIV + args.chunk - 1) / args.chunk) * args.chunk;
+        a.tail0 = (uint32_t)(n - min<uint64_t>(tail, n));
         // every segment needs a workgroup that drains it: fewer segments on a small grid
-        a.nseg = min<uint32_t>(kHeads, gridDim.x);
+        a.nseg = min<uint32_t>(kHeads, grid);
         a.seg_size = (a.tail0 + a.nseg - 1) / a.nseg;
     }
 

@@ -79,6 +79,8 @@ struct SolveArgs {
     int locked;                // QUAD solver: locked-candidates pass at fixpoints (SDK_OPT_LOCKED)
     uint32_t* heads;           // QUAD solver: kHeads dequeue heads, one per XCD segment (nullable)
     void* donate;              // QUAD solver, LEX solves: subtree-donation area (solve4_kernel.h, DnCtl first)
+    const uint32_t* n_dev;     // donation kernel: board count read on the device (a phase's list
+                               // length, written by an earlier launch); `n` is then its bound
 };
 
 // per-XCD dequeue: the first n - n/32 boards are cut into kHeads contiguous segments with a

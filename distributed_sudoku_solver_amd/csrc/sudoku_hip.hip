@@ -65,21 +65,55 @@ struct DevBuf {
 namespace sdk {
 // two-phase solve (launch_solve): list the split phase's budget hits, gather them into a
 // dense batch, scatter their answers back
-__global__ void dn_collect_kernel(const int8_t* status, uint64_t n, int8_t code, uint32_t* hits) {
+// A list is a length word and the board indices after it; its length is read on the device
+// (the phases are enqueued without the host).  Collecting a board also copies it (and its
+// first-cell mask) to the list's position in the next phase's dense input: the boards
+// listed are a launch's tail, a few per thousand, so one thread per board does.  n_dev
+// (nullable) bounds n by an earlier list.
+__global__ void dn_collect_kernel(const int8_t* status, uint64_t n, const uint32_t* n_dev, int8_t code,
+                                  uint32_t* list, uint32_t* total, const uint8_t* in, const uint16_t* mask,
+                                  uint64_t in_first, uint64_t in_step, uint8_t* out, uint16_t* out_mask) {
+    if (n_dev) n = min<uint64_t>(n, *n_dev);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        if (status[i] == code) hits[1 + atomicAdd(hits, 1u)] = (uint32_t)i;
+        if (status[i] == code) {
+            const uint32_t k = atomicAdd(list, 1u);
+            list[1 + k] = (uint32_t)i;
+            atomicAdd(total, 1u);
+            const uint8_t* src = in + (in_first + i * in_step) * 81;
+            uint8_t* dst = out + (uint64_t)k * 81;
+            for (int j = 0; j < 81; ++j) dst[j] = src[j];
+            if (mask) out_mask[k] = mask[i];
+        }
 }
-__global__ void dn_gather_kernel(const uint8_t* in, const uint16_t* mask, uint64_t in_first, uint64_t in_step,
-                                 const uint32_t* hits, uint32_t m, uint8_t* out, uint16_t* out_mask) {
-    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
-        const uint64_t j = hits[i];
-        const uint8_t* src = in + (in_first + j * in_step) * 81;
-        if (threadIdx.x < 81) out[(uint64_t)i * 81 + threadIdx.x] = src[threadIdx.x];
-        if (threadIdx.x == 0 && mask) out_mask[i] = mask[j];
+// A phased solve's control words, zeroed in one launch before its first phase: the split
+// phase's dequeue counter and heads, the statistics, both donation launches' control blocks
+// (their epochs set) and list lengths.
+struct DnPrep {
+    uint32_t* counter;
+    uint32_t* heads;
+    uint32_t heads_words;
+    uint32_t* stat;
+    uint32_t* ctl[2];
+    uint32_t epoch[2];
+    uint32_t* list[2];
+};
+__global__ void dn_prep_kernel(DnPrep p) {
+    const uint32_t t = threadIdx.x;
+    if (t == 0) {
+        p.counter[0] = 0;
+        p.list[0][0] = 0;
+        p.list[1][0] = 0;
     }
+    if (p.stat && t < 2) p.stat[t] = 0;
+    if (p.heads)
+        for (uint32_t i = t; i < p.heads_words; i += blockDim.x) p.heads[i] = 0;
+    for (int k = 0; k < 2; ++k)
+        for (uint32_t i = t; i < sizeof(DnCtl) / 4; i += blockDim.x) p.ctl[k][i] = i == 0 ? p.epoch[k] : 0u;
 }
-__global__ void dn_scatter_kernel(const uint32_t* hits, uint32_t m, const uint8_t* sub_out, const int8_t* sub_st,
+__global__ void dn_scatter_kernel(const uint32_t* list, const uint8_t* sub_out, const int8_t* sub_st,
                                   const uint64_t* sub_work, bool depth, uint8_t* out, int8_t* status, uint64_t* work) {
+    const uint32_t m = list[0];
+    const uint32_t* hits = list + 1;
     for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
         const uint64_t j = hits[i];
         if (threadIdx.x < 81) out[j * 81 + threadIdx.x] = sub_out[(uint64_t)i * 81 + threadIdx.x];
@@ -112,11 +146,15 @@ struct sdk_ctx {
     DevBuf stack, counter, heads, in, mask, out, status, work, verdict;
     int xcd_heads = 1;             // QUAD: per-XCD dequeue heads (SDK_OPT_XCD_HEADS)
     int donate = 1;                // QUAD, LEX solves: subtree donation (SDK_OPT_DONATE)
-    DevBuf dn;                     // donation area (solve4_kernel.h: DnCtl, records, items, mailboxes)
-    DevBuf hits, dn_in, dn_mask, dn_out, dn_st, dn_work, dn_list;        // the phased solve's tail boards
-    DevBuf dn3_in, dn3_mask, dn3_out, dn3_st, dn3_work, dn3_list;         // ... and its LEX re-solves
-    uint32_t dn_split_boards = 0;  // boards the last phased solve passed to the donation kernel
-    uint32_t dn_lex_boards = 0;    // ... and of those, boards re-solved in LEX order
+    DevBuf dn;                     // two donation areas (solve4_kernel.h: DnCtl, records, items,
+                                   // mailboxes), one per donation phase of a phased solve
+    void* dn_area = nullptr;       // the area of the donation launch being enqueued
+    DevBuf dn_in, dn_mask, dn_out, dn_st, dn_work, dn_list;        // the phased solve's tail boards
+    DevBuf dn3_in, dn3_mask, dn3_out, dn3_st, dn3_work, dn3_list;   // ... and its LEX re-solves
+    DevBuf dn_stat;                // [0] boards the last phased solve passed to the donation
+                                   // kernel, [1] of those, boards re-solved in LEX order
+    bool dn_ran = false;           // the last solve was phased (dn_stat and `delivered` are its)
+    bool timer_hold = false;       // a phased solve is being timed as one span
     int dn_exhaustive = 1;         // phase 2 in MRV count-to-2 order (SDK_OPT_DONATE_MODE)
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
     int dn_blocks_per_cu = 0;      // resident solve4_kernel<true> workgroups per CU (queried once)
@@ -155,7 +193,7 @@ int ensure(DevBuf& b, size_t bytes) {
 // recorded, so a long-running node or drop-in solver holds no per-launch state.
 int timer_begin(sdk_ctx* c, hipEvent_t* stop_out) {
     *stop_out = nullptr;
-    if (!c->timing) return SDK_OK;
+    if (!c->timing || c->timer_hold) return SDK_OK;
     if (c->events_used >= kMaxTimedLaunches) return fail(SDK_EINVAL, "%zu timed launches since sdk_timer_reset", kMaxTimedLaunches);
     if (c->events_used == c->events.size()) {
         hipEvent_t a, b;
@@ -198,12 +236,13 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
 
 
 // dn_phase (QUAD, LEX solves with SDK_OPT_DONATE): 0 plain launch; 1 the split phase (plain
-// kernel, split budget); 2 the donation kernel solve4_kernel<true> on the full resident grid
-// (see launch_solve)
+// kernel, split budget); 2 the donation kernel solve4_kernel<true> on the full resident grid,
+// donation area c->dn_area (see launch_solve).  The phases' control words are zeroed by
+// launch_solve's prep launch.
 int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
                       uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
                       unsigned long long* d_counts, uint64_t in_first, uint64_t in_step, int order, int64_t budget,
-                      int dn_phase) {
+                      int dn_phase, const uint32_t* n_dev = nullptr) {
     // budget: node budget per board for this launch (-1 = the context's SDK_OPT_NODE_BUDGET)
     const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
     if (n == 0) return SDK_OK;
@@ -263,7 +302,8 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     if (rc) return rc;
     rc = ensure(c->counter, 256);
     if (rc) return rc;
-    HIPCALL(hipMemsetAsync(c->counter.p, 0, 8, c->stream));  // word 0 = work counter; words 1.. belong to callers
+    if (dn_phase == 0)   // word 0 = work counter; words 1.. belong to callers
+        HIPCALL(hipMemsetAsync(c->counter.p, 0, 8, c->stream));
     sdk::SolveArgs a;
     a.in = d_in;
     a.mask = d_mask;
@@ -286,31 +326,23 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     a.locked = c->locked;
     a.heads = nullptr;
     a.donate = nullptr;
+    a.n_dev = nullptr;
     unsigned grid_used = grid;
     if (four && !count_mode && dn_phase == 2) {
         // subtree donation: idle waves wait for items while any wave of the grid works, so the
         // grid is the resident one (its occupancy, not waves_per_cu2), whatever the batch size:
         // waves without a board of their own are the helpers
-        if (c->dn.bytes < sdk::kDnBytes) {
-            rc = ensure(c->dn, sdk::kDnBytes);
-            if (rc) return rc;
-            HIPCALL(hipMemsetAsync(c->dn.p, 0, sdk::kDnBytes, c->stream));   // entries of epoch 0
-            c->dn_epoch = 0;
-        }
         if (c->dn_blocks_per_cu <= 0) {
             c->dn_blocks_per_cu = sdk::solve4_dn_blocks_per_cu();
             if (c->dn_blocks_per_cu <= 0) return fail(SDK_EHIP, "occupancy query for the donation kernel failed");
         }
-        if (++c->dn_epoch == 0) {   // 2^32 launches: clear the stale entries once
-            HIPCALL(hipMemsetAsync(c->dn.p, 0, sdk::kDnBytes, c->stream));
-            c->dn_epoch = 1;
-        }
-        // every control word but `delivered` (the solve's total, reset by launch_solve)
-        HIPCALL(hipMemsetAsync(static_cast<char*>(c->dn.p) + 8, 0, sizeof(sdk::DnCtl) - 8, c->stream));
-        HIPCALL(hipMemsetD32Async(static_cast<hipDeviceptr_t>(c->dn.p), (int)c->dn_epoch, 1, c->stream));
-        a.donate = c->dn.p;
-        // helpers: 16 waves per board beyond 64, up to the resident grid (a few tail boards do
-        // not need thousands of idle waves registering and polling)
+        a.donate = c->dn_area;
+        // the boards: a list length on the device (n bounds it), one per dequeue on the
+        // area's own counter
+        a.n_dev = n_dev;
+        a.chunk = 1;
+        a.next = &static_cast<sdk::DnCtl*>(c->dn_area)->next;
+        // the resident grid; the kernel keeps 64 + 16 waves per board of it (solve4_kernel)
         grid_used = (unsigned)std::max<uint64_t>(
             1, std::min<uint64_t>({(uint64_t)c->cus * (uint64_t)std::min(c->dn_blocks_per_cu, c->waves_per_cu2),
                                    (uint64_t)sdk::kDnMbox, 64ull + 16ull * (uint64_t)n}));
@@ -320,10 +352,11 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
             a.stack = static_cast<uint32_t*>(c->stack.p);
         }
     }
-    if (four && c->xcd_heads) {
+    if (four && c->xcd_heads && dn_phase != 2) {
         rc = ensure(c->heads, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t));
         if (rc) return rc;
-        HIPCALL(hipMemsetAsync(c->heads.p, 0, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t), c->stream));
+        if (dn_phase == 0)
+            HIPCALL(hipMemsetAsync(c->heads.p, 0, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t), c->stream));
         a.heads = static_cast<uint32_t*>(c->heads.p);
     }
     hipEvent_t stop;
@@ -351,54 +384,88 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
 // completions for (or cannot decide within the budget) are solved a third time in LEX
 // order with donation.  Results are the ones a single slot finds (same boards and
 // statuses; `work` adds up the phases and parts).
-int dn_list(sdk_ctx* c, const int8_t* d_status, uint64_t n, int8_t code, uint32_t* m) {
-    HIPCALL(hipMemsetAsync(c->hits.p, 0, sizeof(uint32_t), c->stream));
+//
+// Every phase is enqueued at once, without the host: the lists of boards a phase passes
+// on live on the device (length word first), and the gather, donation and scatter kernels
+// read their lengths there (an empty list costs a few microseconds of launches).  The
+// phase buffers are sized for every board of the call, up to kDnCapBoards boards per
+// phased pass; larger calls run in passes of that many.
+constexpr uint64_t kDnCapBoards = 1ull << 24;
+
+// list the boards of status[0, n) (n bounded by *n_dev when given) that carry `code` into
+// `list` (its length zeroed by the prep launch), copying them to (buf_in, buf_mask)
+int dn_collect(sdk_ctx* c, const int8_t* d_status, uint64_t n, const uint32_t* n_dev, int8_t code, DevBuf& list,
+               int stat, const uint8_t* d_in, const uint16_t* d_mask, uint64_t in_first, uint64_t in_step,
+               DevBuf& buf_in, DevBuf& buf_mask) {
+    int rc;
+    if ((rc = ensure(buf_in, (size_t)n * 81)) || (d_mask && (rc = ensure(buf_mask, (size_t)n * 2)))) return rc;
     sdk::dn_collect_kernel<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)c->cus * 8)),
-                             256, 0, c->stream>>>(d_status, n, code, static_cast<uint32_t*>(c->hits.p));
+                             256, 0, c->stream>>>(d_status, n, n_dev, code, static_cast<uint32_t*>(list.p),
+                                                  static_cast<uint32_t*>(c->dn_stat.p) + stat, d_in, d_mask, in_first,
+                                                  in_step, static_cast<uint8_t*>(buf_in.p),
+                                                  static_cast<uint16_t*>(d_mask ? buf_mask.p : nullptr));
     HIPCALL(hipGetLastError());
-    HIPCALL(hipMemcpyAsync(m, c->hits.p, sizeof *m, hipMemcpyDeviceToHost, c->stream));
-    HIPCALL(hipStreamSynchronize(c->stream));
     return SDK_OK;
 }
 
-// gather the listed boards of (d_in, d_mask) into buf_in/buf_mask, solve them with the
-// donation kernel (order), scatter the answers into (d_out, d_status, d_work)
-int dn_resolve(sdk_ctx* c, uint32_t m, const uint8_t* d_in, const uint16_t* d_mask, uint64_t in_first,
-               uint64_t in_step, uint8_t* d_out, int8_t* d_status, uint64_t* d_work, int order, int64_t budget,
-               DevBuf& buf_in, DevBuf& buf_mask, DevBuf& buf_out, DevBuf& buf_st, DevBuf& buf_work, DevBuf& list) {
+// solve the (at most cap) boards `list` collected into buf_in/buf_mask with the donation
+// kernel (order) in donation area `area`, scatter the answers into (d_out, d_status, d_work)
+int dn_resolve(sdk_ctx* c, uint64_t cap, const DevBuf& list, int area, bool has_mask, uint8_t* d_out,
+               int8_t* d_status, uint64_t* d_work, int order, int64_t budget, DevBuf& buf_in, DevBuf& buf_mask,
+               DevBuf& buf_out, DevBuf& buf_st, DevBuf& buf_work) {
     int rc;
-    if ((rc = ensure(buf_in, (size_t)m * 81)) || (rc = ensure(buf_out, (size_t)m * 81)) || (rc = ensure(buf_st, m)) ||
-        (d_work && (rc = ensure(buf_work, (size_t)m * 8))) || (d_mask && (rc = ensure(buf_mask, (size_t)m * 2))) ||
-        (rc = ensure(list, ((size_t)m + 1) * sizeof(uint32_t))))
+    if ((rc = ensure(buf_out, (size_t)cap * 81)) || (rc = ensure(buf_st, cap)) ||
+        (d_work && (rc = ensure(buf_work, (size_t)cap * 8))))
         return rc;
-    // keep this phase's list: the next phase lists into c->hits again
-    HIPCALL(hipMemcpyAsync(list.p, c->hits.p, ((size_t)m + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
-    const uint32_t* idx = static_cast<const uint32_t*>(list.p) + 1;
-    const unsigned g = (unsigned)std::min<uint64_t>(m, (uint64_t)c->cus * 16);
-    sdk::dn_gather_kernel<<<g, 128, 0, c->stream>>>(d_in, d_mask, in_first, in_step, idx, m,
-                                                    static_cast<uint8_t*>(buf_in.p),
-                                                    static_cast<uint16_t*>(d_mask ? buf_mask.p : nullptr));
-    HIPCALL(hipGetLastError());
-    if ((rc = launch_solve_once(c, static_cast<uint8_t*>(buf_in.p), d_mask ? static_cast<uint16_t*>(buf_mask.p) : nullptr,
-                                static_cast<uint8_t*>(buf_out.p), static_cast<int8_t*>(buf_st.p),
-                                d_work ? static_cast<uint64_t*>(buf_work.p) : nullptr, m, 0, 0, nullptr, nullptr, 0, 1,
-                                order, budget, 2)))
+    const uint32_t* lst = static_cast<const uint32_t*>(list.p);
+    uint8_t* in = static_cast<uint8_t*>(buf_in.p);
+    uint16_t* mask = has_mask ? static_cast<uint16_t*>(buf_mask.p) : nullptr;
+    uint8_t* out = static_cast<uint8_t*>(buf_out.p);
+    int8_t* st = static_cast<int8_t*>(buf_st.p);
+    uint64_t* work = d_work ? static_cast<uint64_t*>(buf_work.p) : nullptr;
+    c->dn_area = static_cast<char*>(c->dn.p) + (size_t)area * sdk::kDnBytes;
+    if ((rc = launch_solve_once(c, in, mask, out, st, work, cap, 0, 0, nullptr, nullptr, 0, 1, order, budget, 2, lst)))
         return rc;
     if (order == SDK_ORDER_MRV_UNIQUE) {
         // boards with several completions (or undecided): LEX order, donation again
-        uint32_t m3 = 0;
-        if ((rc = dn_list(c, static_cast<int8_t*>(buf_st.p), m, (int8_t)sdk::kDnRetryLex, &m3))) return rc;
-        c->dn_lex_boards = m3;
-        if (m3 && (rc = dn_resolve(c, m3, static_cast<uint8_t*>(buf_in.p), d_mask ? static_cast<uint16_t*>(buf_mask.p) : nullptr,
-                                   0, 1, static_cast<uint8_t*>(buf_out.p), static_cast<int8_t*>(buf_st.p),
-                                   d_work ? static_cast<uint64_t*>(buf_work.p) : nullptr, SDK_ORDER_LEX, budget,
-                                   c->dn3_in, c->dn3_mask, c->dn3_out, c->dn3_st, c->dn3_work, c->dn3_list)))
+        if ((rc = dn_collect(c, st, cap, lst, (int8_t)sdk::kDnRetryLex, c->dn3_list, 1, in, mask, 0, 1, c->dn3_in,
+                             c->dn3_mask)) ||
+            (rc = dn_resolve(c, cap, c->dn3_list, 1, has_mask, out, st, work, SDK_ORDER_LEX, budget, c->dn3_in,
+                             c->dn3_mask, c->dn3_out, c->dn3_st, c->dn3_work)))
             return rc;
     }
-    sdk::dn_scatter_kernel<<<g, 128, 0, c->stream>>>(idx, m, static_cast<const uint8_t*>(buf_out.p),
-                                                     static_cast<const int8_t*>(buf_st.p),
-                                                     d_work ? static_cast<const uint64_t*>(buf_work.p) : nullptr,
-                                                     c->work_rounds == SDK_WORK_DEPTH, d_out, d_status, d_work);
+    const unsigned g = (unsigned)std::min<uint64_t>(cap, (uint64_t)c->cus * 16);
+    sdk::dn_scatter_kernel<<<g, 128, 0, c->stream>>>(lst, out, st, work, c->work_rounds == SDK_WORK_DEPTH, d_out,
+                                                     d_status, d_work);
+    HIPCALL(hipGetLastError());
+    return SDK_OK;
+}
+
+// zero a phased pass's control words in one launch (sdk::dn_prep_kernel)
+int dn_prep(sdk_ctx* c, uint64_t cap, bool first_pass) {
+    int rc;
+    if (c->dn.bytes < 2 * sdk::kDnBytes || c->dn_epoch > 0xFFFFFF00u) {
+        // entries of epoch 0 (and, after 2^32 launches, the stale ones cleared once)
+        if ((rc = ensure(c->dn, 2 * sdk::kDnBytes))) return rc;
+        HIPCALL(hipMemsetAsync(c->dn.p, 0, 2 * sdk::kDnBytes, c->stream));
+        c->dn_epoch = 0;
+    }
+    if ((rc = ensure(c->dn_stat, 256)) || (rc = ensure(c->counter, 256)) ||
+        (rc = ensure(c->heads, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t))) ||
+        (rc = ensure(c->dn_list, (cap + 1) * sizeof(uint32_t))) || (rc = ensure(c->dn3_list, (cap + 1) * sizeof(uint32_t))))
+        return rc;
+    sdk::DnPrep p{};
+    p.counter = static_cast<uint32_t*>(c->counter.p);
+    p.heads = c->xcd_heads ? static_cast<uint32_t*>(c->heads.p) : nullptr;
+    p.heads_words = (sdk::kHeads + 1) * sdk::kHeadStride;
+    p.stat = first_pass ? static_cast<uint32_t*>(c->dn_stat.p) : nullptr;   // statistics add up over passes
+    for (int k = 0; k < 2; ++k) {
+        p.ctl[k] = reinterpret_cast<uint32_t*>(static_cast<char*>(c->dn.p) + (size_t)k * sdk::kDnBytes);
+        p.epoch[k] = ++c->dn_epoch;
+    }
+    p.list[0] = static_cast<uint32_t*>(c->dn_list.p);
+    p.list[1] = static_cast<uint32_t*>(c->dn3_list.p);
+    sdk::dn_prep_kernel<<<1, 256, 0, c->stream>>>(p);
     HIPCALL(hipGetLastError());
     return SDK_OK;
 }
@@ -410,26 +477,37 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     const int eff_order = order >= 0 ? order : c->order;
     const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
     const uint64_t split = c->donate == 1 ? kDnSplitDefault : (uint64_t)c->donate;
-    c->dn_split_boards = 0;
-    c->dn_lex_boards = 0;
     const bool two_phase = n > 0 && !count_mode && c->donate && c->solver == SDK_SOLVER_QUAD &&
                            eff_order == SDK_ORDER_LEX && d_out && d_status && (node_budget == 0 || node_budget > split);
+    c->dn_ran = two_phase;
     if (!two_phase)
         return launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, count_mode, limit, d_count, d_counts,
                                  in_first, in_step, order, budget, 0);
-    int rc;
-    if ((rc = ensure(c->hits, (n + 1) * sizeof(uint32_t)))) return rc;
-    if (c->dn.p) HIPCALL(hipMemsetAsync(static_cast<char*>(c->dn.p) + 4, 0, 4, c->stream));   // `delivered`
-    if ((rc = launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, 0, 0, nullptr, nullptr, in_first, in_step,
-                                order, (int64_t)split, 1)))
-        return rc;
-    uint32_t m = 0;
-    if ((rc = dn_list(c, d_status, n, (int8_t)-2, &m))) return rc;
-    c->dn_split_boards = m;
-    if (m == 0) return SDK_OK;
-    return dn_resolve(c, m, d_in, d_mask, in_first, in_step, d_out, d_status, d_work,
-                      c->dn_exhaustive ? SDK_ORDER_MRV_UNIQUE : SDK_ORDER_LEX, (int64_t)node_budget, c->dn_in,
-                      c->dn_mask, c->dn_out, c->dn_st, c->dn_work, c->dn_list);
+    // SDK_OPT_TIMING: the phases of one solve are one timed span
+    hipEvent_t stop;
+    int rc = timer_begin(c, &stop);
+    if (rc) return rc;
+    c->timer_hold = true;
+    const uint64_t step = in_step ? in_step : 1;
+    for (uint64_t b0 = 0; b0 < n && !rc; b0 += kDnCapBoards) {
+        const uint64_t m = std::min<uint64_t>(n - b0, kDnCapBoards);
+        uint8_t* out = d_out + b0 * 81;
+        int8_t* st = d_status + b0;
+        uint64_t* work = d_work ? d_work + b0 : nullptr;
+        const uint16_t* mask = d_mask ? d_mask + b0 : nullptr;
+        const uint64_t first = in_first + b0 * step;
+        (void)((rc = dn_prep(c, m, b0 == 0)) ||
+               (rc = launch_solve_once(c, d_in, mask, out, st, work, m, 0, 0, nullptr, nullptr, first, step, order,
+                                       (int64_t)split, 1)) ||
+               (rc = dn_collect(c, st, m, nullptr, (int8_t)-2, c->dn_list, 0, d_in, mask, first, step, c->dn_in,
+                                c->dn_mask)) ||
+               (rc = dn_resolve(c, m, c->dn_list, 0, mask != nullptr, out, st, work,
+                                c->dn_exhaustive ? SDK_ORDER_MRV_UNIQUE : SDK_ORDER_LEX, (int64_t)node_budget, c->dn_in,
+                                c->dn_mask, c->dn_out, c->dn_st, c->dn_work)));
+    }
+    c->timer_hold = false;
+    if (rc) return rc;
+    return timer_end(c, stop);
 }
 
 // Deterministic breadth-first frontier of one board, left in c->fr_a.
@@ -712,7 +790,7 @@ int sdk_destroy(sdk_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf* b : {&c->dn, &c->hits, &c->dn_in, &c->dn_mask, &c->dn_out, &c->dn_st, &c->dn_work, &c->dn_list,
+    for (DevBuf* b : {&c->dn, &c->dn_stat, &c->dn_in, &c->dn_mask, &c->dn_out, &c->dn_st, &c->dn_work, &c->dn_list,
                       &c->dn3_in, &c->dn3_mask, &c->dn3_out, &c->dn3_st, &c->dn3_work, &c->dn3_list,
                       &c->stack, &c->counter, &c->heads, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
                       &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status,
@@ -817,6 +895,20 @@ extern "C" int sdk_debug_dn_ctl(sdk_ctx* c, uint32_t* out16) {
     return SDK_OK;
 }
 
+namespace {
+// a phased solve's board counts (dn_stat) wait for it on the context's stream
+int read_dn_stat(sdk_ctx* c, int k, int64_t* value) {
+    *value = 0;
+    if (!c->dn_ran || !c->dn_stat.p) return SDK_OK;
+    HIPCALL(hipSetDevice(c->device));
+    uint32_t v = 0;
+    HIPCALL(hipMemcpyAsync(&v, static_cast<uint32_t*>(c->dn_stat.p) + k, sizeof v, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    *value = v;
+    return SDK_OK;
+}
+}  // namespace
+
 int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
     if (!c || !value) return fail(SDK_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lk(c->mu);
@@ -835,18 +927,21 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_LOCKED: *value = c->locked; return SDK_OK;
         case SDK_OPT_XCD_HEADS: *value = c->xcd_heads; return SDK_OK;
         case SDK_OPT_DONATE: *value = c->donate; return SDK_OK;
-        case SDK_OPT_SPLIT_BOARDS: *value = c->dn_split_boards; return SDK_OK;
+        case SDK_OPT_SPLIT_BOARDS: return read_dn_stat(c, 0, value);
         case SDK_OPT_DONATE_MODE: *value = c->dn_exhaustive; return SDK_OK;
-        case SDK_OPT_LEX_BOARDS: *value = c->dn_lex_boards; return SDK_OK;
+        case SDK_OPT_LEX_BOARDS: return read_dn_stat(c, 1, value);
         case SDK_OPT_DONATED: {
-            // items handed out by the last donating launch (waits for it on the context's stream)
+            // items handed out by the last phased solve's donation launches (of its last
+            // kDnCapBoards-board pass; waits for it on the context's stream)
             *value = 0;
-            if (!c->dn.p || c->dn_epoch == 0 || c->dn_split_boards == 0) return SDK_OK;
+            if (!c->dn.p || c->dn_epoch == 0 || !c->dn_ran) return SDK_OK;
             HIPCALL(hipSetDevice(c->device));
-            sdk::DnCtl h{};
-            HIPCALL(hipMemcpyAsync(&h, c->dn.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+            sdk::DnCtl h[2];
+            for (int k = 0; k < 2; ++k)
+                HIPCALL(hipMemcpyAsync(&h[k], static_cast<char*>(c->dn.p) + (size_t)k * sdk::kDnBytes, sizeof h[k],
+                                       hipMemcpyDeviceToHost, c->stream));
             HIPCALL(hipStreamSynchronize(c->stream));
-            *value = (int64_t)h.delivered;
+            *value = (int64_t)h[0].delivered + (int64_t)h[1].delivered;
             return SDK_OK;
         }
         case SDK_OPT_TIMER_EVENTS: *value = (int64_t)c->events.size(); return SDK_OK;

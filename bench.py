@@ -91,7 +91,7 @@ def parse_args():
                     help="per-lane reference-DFS leg on a C2 prefix (rank 0, N=1; 0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
                     help="watchdog for the side legs: print what was measured and exit")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02", "pmc_c4.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r03", "pmc_c4.json"),
                     help="per-launch PMC figures of the C4 solve kernel and the C3 checker from rocprofv3 passes "
                          "of this bench at its default sizes (tools/pmc_c4.sh); '' = report traffic null")
     ap.add_argument("--engine-factory", default="", help=argparse.SUPPRESS)
@@ -718,6 +718,9 @@ def main():
         "traffic": srec["traffic_bytes"] if srec else None,
         "traffic_note": srec.get("traffic_note") if srec else None,
         "traffic_source": (os.path.relpath(args.pmc_summary, ROOT) if srec else None),
+        # the counters themselves beside the calibrated figure: the raw write is ~1.37x the 82 B
+        # per puzzle because each 81-B record is written on its own (solver traffic)
+        "traffic_raw": srec.get("traffic_raw") if srec else None,
         "kernel": solve_kernel,
         "avg_kernel_ms": avg_kernel_s * 1000.0,
         "note": "the search is VALU-issue / LDS-latency bound: see roofline.valu; HBM fraction reported "
@@ -734,6 +737,7 @@ def main():
             "valu_active_per_wave_cycle": srec.get("valu_active_per_wave_cycle"),
             "lds_insts_per_puzzle": srec.get("lds_insts", 0) / n,
             "lds_bank_conflict_cycles": srec.get("lds_bank_conflict"),
+            "stalls": srec.get("stalls"),
             "source": os.path.relpath(args.pmc_summary, ROOT),
         }
     result = {

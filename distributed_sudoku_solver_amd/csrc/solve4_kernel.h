@@ -1197,8 +1197,24 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
 
 template <int HI>
 __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c) {
+#if SDK_SOLVE4_STATIC == 1   // experiment: boards dealt round robin to the slots, no dequeue atomics
+    b.bidx = b.bend == 0u ? blockIdx.x * 4u + (uint32_t)w.half * 2u + HI : b.bidx + gridDim.x * 4u;
+    b.bend = 1u;
+    if (false) {
+#elif SDK_SOLVE4_STATIC == 2   // experiment: one contiguous block of boards per slot, no atomics
+    if (b.bend == 0u) {
+        const uint64_t S = (uint64_t)gridDim.x * 4u, s = blockIdx.x * 4u + (uint32_t)w.half * 2u + HI;
+        b.bidx = (uint32_t)(a.n * s / S);
+        b.bend = (uint32_t)(a.n * (s + 1) / S);
+        if (b.bidx >= b.bend) b.bidx = (uint32_t)a.n;
+    } else if (++b.bidx >= b.bend) {
+        b.bidx = (uint32_t)a.n;
+    }
+    if (false) {
+#else
     ++b.bidx;
     if (b.bidx >= b.bend) {
+#endif
         if (a.heads) {
             // XCD-local segment (see kHeads), then the shared tail: straight-line code, no
             // segment-walking loop (its control flow alone made the allocator spill the

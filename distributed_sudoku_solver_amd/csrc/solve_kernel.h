@@ -87,7 +87,10 @@ struct SolveArgs {
 // head each, workgroup g takes chunks of segment g % kHeads (the XCD the round-robin
 // dispatch put it on) and, once that is drained, of the shared tail (one more head);
 // heads kHeadStride words apart (own cache lines)
-constexpr int kHeads = 8;
+#ifndef SDK_HEADS
+#define SDK_HEADS 8
+#endif
+constexpr int kHeads = SDK_HEADS;   // a multiple of 8: segment g % kHeads stays on one XCD
 constexpr int kHeadStride = 64;
 
 __device__ __forceinline__ uint32_t cell_init(uint32_t v) {

@@ -33,8 +33,30 @@ __global__ __launch_bounds__(64) void fetch_kernel(const unsigned char* __restri
     }
 }
 
+// The same records and bytes, output written 16 records per wave with 16-B stores: a
+// group's 1296 B start 16-B aligned and are covered by 81 dwordx4 stores (lanes 0..63, then
+// 0..16), so every output line is written whole, at once.  Mode 1 of main: what WRITE_SIZE
+// reports when the 81-B records are not written one by one.
+__global__ __launch_bounds__(64) void fetch_kernel_wide(const unsigned char* __restrict__ in,
+                                                        unsigned char* __restrict__ out,
+                                                        unsigned char* __restrict__ status, unsigned n) {
+    const unsigned groups = n / 16;
+    for (unsigned g = blockIdx.x; g < groups; g += gridDim.x) {
+        const uint4* src = reinterpret_cast<const uint4*>(in + (size_t)g * 1296);
+        uint4* dst = reinterpret_cast<uint4*>(out + (size_t)g * 1296);
+        for (unsigned k = threadIdx.x; k < 81; k += 64) {
+            uint4 v = src[k];
+            v.x += 0x01010101u; v.y += 0x01010101u; v.z += 0x01010101u; v.w += 0x01010101u;
+            dst[k] = v;
+        }
+        if (threadIdx.x < 4)
+            reinterpret_cast<unsigned*>(status + (size_t)g * 16)[threadIdx.x] = 0x01010101u;
+    }
+}
+
 int main(int argc, char** argv) {
     const unsigned n = argc > 1 ? (unsigned)atoi(argv[1]) : 10000000u;
+    const int mode = argc > 2 ? atoi(argv[2]) : 0;   // 0: the solvers' byte pattern, 1: wide stores
     unsigned char *in, *out, *status;
     CK(hipMalloc(&in, (size_t)n * 81));
     CK(hipMalloc(&out, (size_t)n * 81));
@@ -48,12 +70,15 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&b));
     for (int rep = 0; rep < 3; ++rep) {
         CK(hipEventRecord(a));
-        fetch_kernel<<<grid, 64>>>(in, out, status, n);
+        if (mode == 1)
+            fetch_kernel_wide<<<grid, 64>>>(in, out, status, n);
+        else
+            fetch_kernel<<<grid, 64>>>(in, out, status, n);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms = 0;
         CK(hipEventElapsedTime(&ms, a, b));
-        printf("fetch_kernel n=%u records: %.3f ms, algorithmic %.1f MB read + %.1f MB written\n", n, ms,
+        printf("fetch_kernel mode %d n=%u records: %.3f ms, algorithmic %.1f MB read + %.1f MB written\n", mode, n, ms,
                n * 81 / 1e6, n * 82 / 1e6);
     }
     return 0;

@@ -12,8 +12,10 @@ from distributed_sudoku_solver_amd import SudokuEngine, synth, _lib as L  # noqa
 
 b15 = synth.SEEDS17["S1"][:-9] + "0" * 9
 b14 = synth.parse(b15[:63] + "000100000" + "0" * 9)     # bench.py c5_board("14")
+solver = sys.argv[1] if len(sys.argv) > 1 else "quad"   # quad: expand4_kernel; halfwave: expand_kernel
 with SudokuEngine(0) as eng:
+    eng.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD if solver == "quad" else L.SDK_SOLVER_HALFWAVE)
     for target in (1_000_000, 1_000_000, 1_000_000):
         t0 = time.perf_counter()
         size, leaves = eng.frontier_build(b14, target=target)
-        print(f"target {target}: {size} boards, {leaves} leaves, {1e3 * (time.perf_counter() - t0):.2f} ms", flush=True)
+        print(f"{solver} target {target}: {size} boards, {leaves} leaves, {1e3 * (time.perf_counter() - t0):.2f} ms", flush=True)

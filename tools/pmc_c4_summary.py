@@ -23,6 +23,8 @@ from collections import defaultdict
 CAL_RECORDS = 10_000_000
 C4_PUZZLES = 10_000_000
 C3_BOARDS = 100_000_000
+MIN_PUZZLES = 1_048_576
+HARD_PUZZLES = 100_000
 
 
 def load(d, tag):
@@ -32,6 +34,10 @@ def load(d, tag):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"].split("(")[0].strip()
+                if k.startswith("void "):
+                    k = k[5:]
+                k = k.replace("solve4_kernel<false>", "solve4_kernel").replace("solve4_kernel<true>",
+                                                                              "solve4_kernel_donate")
                 per[k][row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
     return {k: {c: list(v.values()) for c, v in cs.items()} for k, cs in per.items()}
 
@@ -47,26 +53,66 @@ def kernel_like(table, prefix):
     return None
 
 
+SQW_FIELDS = ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS",
+              "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VMEM")
+
+
+def stall_breakdown(g):
+    """SQ_WAIT_* / SQ_ACTIVE_INST_* per wave-cycle (all in quad-cycles; WAIT_ANY + WAIT_INST_ANY +
+    ACTIVE_INST_ANY ~= WAVE_CYCLES, MI355X_MICROARCH.md rocprofv3 PMC slots)."""
+    wc = g.get("SQ_WAVE_CYCLES")
+    if not wc:
+        return None
+    return {c.lower().replace("sq_", "") + "_per_wave_cycle": g[c] / wc for c in SQW_FIELDS if g.get(c) is not None}
+
+
+def sq_fields(rec, s, sw):
+    if s:
+        g = {c: avg(v) for c, v in s.items()}
+        rec.update(valu_insts=g.get("SQ_INSTS_VALU"), salu_insts=g.get("SQ_INSTS_SALU"),
+                   lds_insts=g.get("SQ_INSTS_LDS"), lds_bank_conflict=g.get("SQ_LDS_BANK_CONFLICT"),
+                   lds_idx_active=g.get("SQ_LDS_IDX_ACTIVE"), waves=g.get("SQ_WAVES"),
+                   valu_active_per_wave_cycle=(g["SQ_ACTIVE_INST_VALU"] / g["SQ_WAVE_CYCLES"]
+                                               if g.get("SQ_WAVE_CYCLES") else None))
+        u = rec["units_per_launch"]
+        rec.update(valu_insts_per_unit=g.get("SQ_INSTS_VALU", 0) / u, lds_insts_per_unit=g.get("SQ_INSTS_LDS", 0) / u)
+    if sw:
+        rec["stalls"] = stall_breakdown({c: avg(v) for c, v in sw.items()})
+
+
+def calibration(d, tag, records):
+    f, w = load(d, f"{tag}_fetch"), load(d, f"{tag}_write")
+    kf, kw = kernel_like(f, "fetch_kernel"), kernel_like(w, "fetch_kernel")
+    if not kf or not kw:
+        return {}
+    fb = avg(f[kf]["FETCH_SIZE"]) * 1024
+    wb = avg(w[kw]["WRITE_SIZE"]) * 1024
+    return {"records": records, "kernel": kf, "fetch_size_bytes": fb, "write_size_bytes": wb,
+            "read_correction": records * 81 / fb, "write_correction": records * 82 / wb}
+
+
 def main(d):
     out = {}
-    cal_f, cal_w = load(d, "cal_fetch"), load(d, "cal_write")
-    kc = kernel_like(cal_f, "fetch_kernel")
-    cal = {}
-    if kc:
-        fb = avg(cal_f[kc]["FETCH_SIZE"]) * 1024
-        wb = avg(cal_w[kernel_like(cal_w, "fetch_kernel")]["WRITE_SIZE"]) * 1024
-        cal = {"records": CAL_RECORDS, "fetch_size_bytes": fb, "write_size_bytes": wb,
-               "read_correction": CAL_RECORDS * 81 / fb, "write_correction": CAL_RECORDS * 82 / wb}
+    cal = calibration(d, "cal", CAL_RECORDS)
+    if cal:
         out["calibration"] = cal
-    for tag, units, prefix, read_corr, write_corr, note in (
+    calw = calibration(d, "calw", CAL_RECORDS)
+    if calw:
+        calw["note"] = ("the same 10M records and bytes, output written 16 records (1296 B, 16-B aligned) at a "
+                        "time with 16-B stores")
+        out["calibration_wide_stores"] = calw
+    for tag, units, prefix, read_corr, write_corr, note, algo in (
             ("c4", C4_PUZZLES, "sdk::solve", cal.get("read_correction"), cal.get("write_correction"),
              "FETCH/WRITE_SIZE scaled by tools/fetch_calib's algorithmic/counter ratios for the solvers' "
-             "byte-load/byte-store pattern"),
+             "byte-load/byte-store pattern", (81, 82)),
             ("c3", C3_BOARDS, "sdk::check_kernel", 2.0, 1.0,
-             "2 x FETCH_SIZE (gfx950: FETCH_SIZE reports half of a 16-B/lane streaming read) + WRITE_SIZE")):
-        f, w, sq = load(d, f"{tag}_fetch"), load(d, f"{tag}_write"), load(d, f"{tag}_sq")
-        for k in sorted(set(f) | set(sq)):
-            if not k.startswith(prefix):
+             "2 x FETCH_SIZE (gfx950: FETCH_SIZE reports half of a 16-B/lane streaming read) + WRITE_SIZE", (81, 1)),
+            ("min", MIN_PUZZLES, "sdk::solve4_kernel", None, None, None, None),
+            ("hard", HARD_PUZZLES, "sdk::solve4_kernel", None, None, None, None)):
+        f, w = load(d, f"{tag}_fetch"), load(d, f"{tag}_write")
+        sq, sqw = load(d, f"{tag}_sq"), load(d, f"{tag}_sqw")
+        for k in sorted(set(f) | set(sq) | set(sqw)):
+            if not k.startswith(prefix) or k.endswith("_donate"):
                 continue
             if tag == "c3" and k != "sdk::check_kernel":
                 continue
@@ -76,16 +122,14 @@ def main(d):
             if fb is not None and wb is not None and read_corr and write_corr:
                 rec.update(dispatches=len(f[k]["FETCH_SIZE"]), fetch_size_bytes=fb * 1024,
                            write_size_bytes=wb * 1024, read_correction=read_corr, write_correction=write_corr,
-                           traffic_bytes=fb * 1024 * read_corr + wb * 1024 * write_corr, traffic_note=note)
-            s = sq.get(k, {})
-            if s:
-                g = {c: avg(v) for c, v in s.items()}
-                rec.update(valu_insts=g.get("SQ_INSTS_VALU"), salu_insts=g.get("SQ_INSTS_SALU"),
-                           lds_insts=g.get("SQ_INSTS_LDS"), lds_bank_conflict=g.get("SQ_LDS_BANK_CONFLICT"),
-                           lds_idx_active=g.get("SQ_LDS_IDX_ACTIVE"), waves=g.get("SQ_WAVES"),
-                           valu_active_per_wave_cycle=(g["SQ_ACTIVE_INST_VALU"] / g["SQ_WAVE_CYCLES"]
-                                                       if g.get("SQ_WAVE_CYCLES") else None))
-            out[k] = rec
+                           traffic_bytes=fb * 1024 * read_corr + wb * 1024 * write_corr, traffic_note=note,
+                           traffic_raw={"fetch_size_bytes": fb * 1024, "write_size_bytes": wb * 1024,
+                                        "algorithmic_read_bytes": algo[0] * units,
+                                        "algorithmic_write_bytes": algo[1] * units,
+                                        "raw_write_over_algorithmic": wb * 1024 / (algo[1] * units)})
+            sq_fields(rec, sq.get(k, {}), sqw.get(k, {}))
+            key = k if tag in ("c4", "c3") else f"{k}@{tag}"
+            out[key] = rec
     with open(os.path.join(d, "pmc_c4.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     for k, v in out.items():

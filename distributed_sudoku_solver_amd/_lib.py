@@ -44,6 +44,7 @@ SDK_OPT_DONATED = 16
 SDK_OPT_SPLIT_BOARDS = 17
 SDK_OPT_DONATE_MODE = 18
 SDK_OPT_LEX_BOARDS = 19
+SDK_OPT_DONATE_MAX = 20
 SDK_CHECK_REG1 = 0
 SDK_CHECK_REG2 = 1
 SDK_CHECK_GLDS2 = 2

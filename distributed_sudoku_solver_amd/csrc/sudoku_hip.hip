@@ -156,6 +156,7 @@ struct sdk_ctx {
     bool dn_ran = false;           // the last solve was phased (dn_stat and `delivered` are its)
     bool timer_hold = false;       // a phased solve is being timed as one span
     int dn_exhaustive = 1;         // phase 2 in MRV count-to-2 order (SDK_OPT_DONATE_MODE)
+    int64_t dn_max = 1 << 19;      // largest batch solved in phases (SDK_OPT_DONATE_MAX, 0 = any)
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
     int dn_blocks_per_cu = 0;      // resident solve4_kernel<true> workgroups per CU (queried once)
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
@@ -478,7 +479,8 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
     const uint64_t split = c->donate == 1 ? kDnSplitDefault : (uint64_t)c->donate;
     const bool two_phase = n > 0 && !count_mode && c->donate && c->solver == SDK_SOLVER_QUAD &&
-                           eff_order == SDK_ORDER_LEX && d_out && d_status && (node_budget == 0 || node_budget > split);
+                           eff_order == SDK_ORDER_LEX && d_out && d_status && (node_budget == 0 || node_budget > split) &&
+                           (c->dn_max == 0 || (int64_t)n <= c->dn_max);
     c->dn_ran = two_phase;
     if (!two_phase)
         return launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, count_mode, limit, d_count, d_counts,
@@ -862,6 +864,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             return fail(SDK_EINVAL, "SDK_OPT_SPLIT_BOARDS is read-only");
         case SDK_OPT_LEX_BOARDS:
             return fail(SDK_EINVAL, "SDK_OPT_LEX_BOARDS is read-only");
+        case SDK_OPT_DONATE_MAX:
+            if (value < 0) return fail(SDK_EINVAL, "SDK_OPT_DONATE_MAX must be >= 0");
+            c->dn_max = value;
+            return SDK_OK;
         case SDK_OPT_DONATE_MODE:
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "donate mode must be 0 (LEX) or 1 (exhaustive)");
             c->dn_exhaustive = (int)value;
@@ -930,6 +936,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_SPLIT_BOARDS: return read_dn_stat(c, 0, value);
         case SDK_OPT_DONATE_MODE: *value = c->dn_exhaustive; return SDK_OK;
         case SDK_OPT_LEX_BOARDS: return read_dn_stat(c, 1, value);
+        case SDK_OPT_DONATE_MAX: *value = c->dn_max; return SDK_OK;
         case SDK_OPT_DONATED: {
             // items handed out by the last phased solve's donation launches (of its last
             // kDnCapBoards-board pass; waits for it on the context's stream)

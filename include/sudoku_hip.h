@@ -100,6 +100,10 @@ extern "C" {
                                  /* again in LEX with donation; 0: LEX directly          */
 #define SDK_OPT_LEX_BOARDS   19  /* read-only: boards of the last solve's donation phase */
                                  /* that needed the LEX re-solve                         */
+#define SDK_OPT_DONATE_MAX   20  /* largest batch solved in phases with donation         */
+                                 /* (default 2^19; 0 = any size): a larger batch is one  */
+                                 /* launch, where its heavy boards are a small share of  */
+                                 /* the time (1M minimal puzzles: the phases cost 6 %)   */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

@@ -32,6 +32,7 @@ SPLIT = 16    # a small split budget: most searching boards go through the donat
 def _solve(engine, boards, masks=None, donate=SPLIT, budget=None, mode=1):
     engine.set_option(L.SDK_OPT_DONATE, donate)
     engine.set_option(L.SDK_OPT_DONATE_MODE, mode)
+    engine.set_option(L.SDK_OPT_DONATE_MAX, 0)      # phased whatever the batch size
     try:
         out, st, work = engine.solve_batch(boards, masks, want_work=True, budget=budget)
         donated = engine.get_option(L.SDK_OPT_DONATED) if donate else 0
@@ -39,6 +40,7 @@ def _solve(engine, boards, masks=None, donate=SPLIT, budget=None, mode=1):
     finally:
         engine.set_option(L.SDK_OPT_DONATE, 1)
         engine.set_option(L.SDK_OPT_DONATE_MODE, 1)
+        engine.set_option(L.SDK_OPT_DONATE_MAX, 1 << 19)
     if not donate:
         assert split == 0
     return out, st, work, donated
@@ -74,6 +76,29 @@ def test_donation_option_roundtrip(engine):
     for ro in (L.SDK_OPT_DONATED, L.SDK_OPT_SPLIT_BOARDS, L.SDK_OPT_LEX_BOARDS):
         with pytest.raises(L.SudokuHipError):
             engine.set_option(ro, 1)
+    assert engine.get_option(L.SDK_OPT_DONATE_MAX) == 1 << 19
+    with pytest.raises(L.SudokuHipError):
+        engine.set_option(L.SDK_OPT_DONATE_MAX, -1)
+
+
+def test_batch_over_donate_max_is_one_launch(engine):
+    """A batch above SDK_OPT_DONATE_MAX is one launch (its heavy boards never split), with the
+    same answers; at or below it the heavy boards go to the donation phase."""
+    p, s, _ = _heavy_minimal(engine, 20000, 64, seed=5)
+    engine.set_option(L.SDK_OPT_DONATE_MAX, len(p) - 1)
+    try:
+        out, st, _ = engine.solve_batch(p, want_work=True)
+        assert engine.get_option(L.SDK_OPT_SPLIT_BOARDS) == 0
+        assert engine.get_option(L.SDK_OPT_DONATED) == 0
+        assert (st == 1).all() and (out == s).all()
+        engine.set_option(L.SDK_OPT_DONATE_MAX, len(p))
+        engine.set_option(L.SDK_OPT_DONATE, SPLIT)
+        out, st, _ = engine.solve_batch(p, want_work=True)
+        assert engine.get_option(L.SDK_OPT_SPLIT_BOARDS) > 0
+        assert (st == 1).all() and (out == s).all()
+    finally:
+        engine.set_option(L.SDK_OPT_DONATE_MAX, 1 << 19)
+        engine.set_option(L.SDK_OPT_DONATE, 1)
 
 
 def test_easy_batch_takes_one_launch(engine):

@@ -27,6 +27,7 @@ ap.add_argument("--order", default="lex", choices=["mrv_unique", "lex"])
 ap.add_argument("--locked", type=int, default=1, help="QUAD: locked-candidates pass (SDK_OPT_LOCKED: 0 off, 1 root, 2 all nodes)")
 ap.add_argument("--donate", type=int, default=-1, help="QUAD: SDK_OPT_DONATE (default: library default)")
 ap.add_argument("--donate-mode", type=int, default=-1, help="QUAD: SDK_OPT_DONATE_MODE (1 exhaustive, 0 LEX)")
+ap.add_argument("--donate-max", type=int, default=-1, help="QUAD: SDK_OPT_DONATE_MAX (0: phased at any size)")
 args = ap.parse_args()
 
 if args.workload == "minimal":
@@ -54,6 +55,8 @@ with SudokuEngine(0) as eng:
         eng.set_option(L.SDK_OPT_DONATE, args.donate)
     if args.donate_mode >= 0:
         eng.set_option(L.SDK_OPT_DONATE_MODE, args.donate_mode)
+    if args.donate_max >= 0:
+        eng.set_option(L.SDK_OPT_DONATE_MAX, args.donate_max)
     if args.waves_per_cu:
         eng.set_option(wopt, args.waves_per_cu)
     d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)

@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out/static
 log=gpurun_out/static/sweep.log
-for wl in solve17:1250000 solve17:2500000 solve17:10000000 solve30:1000000 minimal:1048576; do
+for wl in ${WORKLOADS:-solve17:1250000 solve17:2500000 solve17:10000000 solve30:1000000 minimal:1048576}; do
   w=${wl%%:*}; n=${wl##*:}
   for v in base ${VARIANTS:-static}; do
     lib=""; [ $v != base ] && lib=$PWD/build/variants/lib_$v.so

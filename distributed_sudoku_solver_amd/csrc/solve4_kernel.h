@@ -652,6 +652,7 @@ static __shared__ uint32_t s_dnpend4; // bit k: s_dnfin4[k] waits; bit 4 + k: sl
 static __shared__ uint32_t s_dnwave4; // bit 0: counted in `finished`, bit 1: registered, bits 8..: polls
 static __shared__ uint32_t s_dnepoch4;
 static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
+static __shared__ uint32_t s_deq4;     // the wave's dequeue stage (next_board4)
 
 // runtime-slot field access (the donation paths run once per loop iteration for any slot)
 __device__ __forceinline__ uint32_t fld_rt(uint32_t w, uint32_t hi) {
@@ -1220,7 +1221,13 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
             // segment-walking loop (its control flow alone made the allocator spill the
             // round's LDS addresses at 72 VGPRs)
             uint32_t base = 0, end = 0;
-            bool drained = (b.active & 2u) != 0u;
+            // the wave's dequeue stage (s_deq4: 0 segment, 1 shared tail, 2 empty) is shared by
+            // its four slots, so a drained head is hit once per wave, not once per slot.  At the
+            // end of a launch every wave meets the drained heads at about the same time and
+            // same-address atomics serialize (~10 ns each): per slot, 28672 failing atomics
+            // on the shared tail cost the 1M 30-clue launch 0.12 ms of its 0.81
+            const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
+            bool drained = stage != 0u, empty = stage == 2u;
             if (!drained) {
                 const uint32_t seg = blockIdx.x % a.nseg;   // the home segment (of this workgroup's XCD)
                 const uint32_t lo = seg * a.seg_size, hi = min(lo + a.seg_size, a.tail0);
@@ -1229,11 +1236,14 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
                 end = hi;
                 drained = base >= hi;
             }
-            if (drained) {
+            if (drained && !empty) {
                 if (w.hl == 0) base = atomicAdd(a.heads + kHeads * kHeadStride, a.tail_chunk);
                 base = a.tail0 + half_first4(w, base);
                 end = (uint32_t)a.n;
+                empty = base >= end;
             }
+            if (empty) base = (uint32_t)a.n;
+            if (w.hl == 0) atomicMax(&s_deq4, empty ? 2u : (drained ? 1u : 0u));
             b.bidx = min(base, (uint32_t)a.n);
             b.bend = min(base + (drained ? a.tail_chunk : a.chunk), end);
             b.active = drained ? 2u : 0u;
@@ -1563,6 +1573,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     __shared__ Slot4 s_slot[4];
     Lane4 w;
     init_lane4(w, s_region, s_in);
+    if (threadIdx.x == 0) s_deq4 = 0u;
 #if SDK_SOLVE4_PROFILE
     if (threadIdx.x < 10) s_prof4[threadIdx.x] = 0;
     __syncthreads();

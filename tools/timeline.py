@@ -58,6 +58,12 @@ def main():
                  "last_dequeue_us": pct(last_deq), "exit_us": pct(us[:, 3]),
                  "drain_us": float(us[:, 3].max() - np.median(last_deq)),
                  "span_us": float(us[:, 3].max())}
+            # per XCD (workgroup % 8: the dispatch's round robin): when its segment work ends
+            xcd = np.arange(g) % 8
+            r["per_xcd"] = {int(k): {"last_dequeue_p50": float(np.median(us[xcd == k, 2])),
+                                     "last_dequeue_max": float(us[xcd == k, 2].max()),
+                                     "exit_p50": float(np.median(us[xcd == k, 3])),
+                                     "exit_max": float(us[xcd == k, 3].max())} for k in range(8)}
             res[str(n)] = r
             print(json.dumps(r), flush=True)
             out = np.empty((n, 81), np.uint8)

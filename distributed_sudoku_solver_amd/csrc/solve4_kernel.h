@@ -1226,24 +1226,38 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
             // end of a launch every wave meets the drained heads at about the same time and
             // same-address atomics serialize (~10 ns each): per slot, 28672 failing atomics
             // on the shared tail cost the 1M 30-clue launch 0.12 ms of its 0.81
-            const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
-            bool drained = stage != 0u, empty = stage == 2u;
-            if (!drained) {
-                const uint32_t seg = blockIdx.x % a.nseg;   // the home segment (of this workgroup's XCD)
-                const uint32_t lo = seg * a.seg_size, hi = min(lo + a.seg_size, a.tail0);
-                if (w.hl == 0) base = atomicAdd(a.heads + seg * kHeadStride, a.chunk);
-                base = lo + half_first4(w, base);
+            const uint32_t seg = blockIdx.x % a.nseg;   // the home segment (of this workgroup's XCD)
+            const uint32_t lo = seg * a.seg_size, hi = min(lo + a.seg_size, a.tail0);
+            // a segment's first chunks are dealt, one per slot of its workgroups, so a launch
+            // does not open with every slot's atomic on eight heads (3,584 each at 28 waves per
+            // CU); the head counts the chunks after them.  A dealt chunk past the segment says
+            // nothing about the other slots' (the wave stage only follows the heads)
+            const uint32_t dealt_base = lo + ((blockIdx.x / a.nseg) * 4u + (uint32_t)w.half * 2u + HI) * a.chunk;
+            const bool dealt_ok = b.bend == 0u && dealt_base < hi;
+            bool drained = false;
+            if (dealt_ok) {
+                base = dealt_base;
                 end = hi;
-                drained = base >= hi;
+            } else {
+                const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
+                drained = stage != 0u;
+                bool empty = stage == 2u;
+                if (!drained) {
+                    const uint32_t dealt = ((gridDim.x - seg + a.nseg - 1u) / a.nseg) * 4u * a.chunk;
+                    if (w.hl == 0) base = atomicAdd(a.heads + seg * kHeadStride, a.chunk);
+                    base = lo + dealt + half_first4(w, base);
+                    end = hi;
+                    drained = base >= hi;
+                }
+                if (drained && !empty) {
+                    if (w.hl == 0) base = atomicAdd(a.heads + kHeads * kHeadStride, a.tail_chunk);
+                    base = a.tail0 + half_first4(w, base);
+                    end = (uint32_t)a.n;
+                    empty = base >= end;
+                }
+                if (empty) base = (uint32_t)a.n;
+                if (w.hl == 0) atomicMax(&s_deq4, empty ? 2u : (drained ? 1u : 0u));
             }
-            if (drained && !empty) {
-                if (w.hl == 0) base = atomicAdd(a.heads + kHeads * kHeadStride, a.tail_chunk);
-                base = a.tail0 + half_first4(w, base);
-                end = (uint32_t)a.n;
-                empty = base >= end;
-            }
-            if (empty) base = (uint32_t)a.n;
-            if (w.hl == 0) atomicMax(&s_deq4, empty ? 2u : (drained ? 1u : 0u));
             b.bidx = min(base, (uint32_t)a.n);
             b.bend = min(base + (drained ? a.tail_chunk : a.chunk), end);
             b.active = drained ? 2u : 0u;

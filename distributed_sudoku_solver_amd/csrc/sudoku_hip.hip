@@ -287,14 +287,15 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     if ((two || four) && !d_status) return fail(SDK_EINVAL, "solve needs a status buffer");
     if ((two || four) && !count_mode && !d_out) return fail(SDK_EINVAL, "solve needs an out buffer");
     const uint64_t slots = (uint64_t)c->cus * (per_wave > 1 ? c->waves_per_cu2 : c->waves_per_cu) * per_wave;
-    // 16 boards per dequeue (fewer when a slot would get < 2 dequeues).  All dequeues hit ONE
-    // counter and same-address atomics serialise at ~10 ns each: below ~16 boards the cheap
-    // C2 boards (1.15 ns per board chip-wide) become dequeue-bound; above it the C4 tail grows
-    // (tools/sweep_chunk.py: chunk 8/16/32/64 = 411/409/404/393M 17-clue puzzles/s).
-    // Count mode uses single boards (subtrees differ by orders of magnitude).
+    // 16 boards per dequeue (fewer when a slot would get < 2 dequeues); 8 for the QUAD solver,
+    // whose dequeues go to per-XCD heads with one stage per wave and dealt first chunks: there
+    // 8 is the fastest at every C4 shard size and on 30-clue boards (round 3,
+    // profiles/r03/sweep_chunk_r03.log: 1.25M 17-clue 1.489 vs 1.557 ms at 16, 10M 10.01 vs
+    // 10.05, 30-clue 1M 0.648 vs 0.676).  Count mode uses single boards (subtrees differ by
+    // orders of magnitude).
     const uint32_t chunk = count_mode ? 1u
         : c->solve_chunk ? (uint32_t)c->solve_chunk
-        : (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, n / (slots * 2)));
+        : (uint32_t)std::min<uint64_t>(per_wave == 4 ? 8 : 16, std::max<uint64_t>(1, n / (slots * 2)));
     const uint64_t want = (n + chunk - 1) / chunk;
     const unsigned grid = (unsigned)std::max<uint64_t>(
         1, std::min<uint64_t>((want + per_wave - 1) / per_wave, slots / per_wave));

@@ -58,7 +58,7 @@ namespace sdk {
 #define SDK_SOLVE4_EXACT_UPD 1        // exact waves also drop the two-hidden-singles test (upd4x)
 #endif
 #ifndef SDK_SOLVE4_TAIL_DIV
-#define SDK_SOLVE4_TAIL_DIV 32        // the shared dequeue tail: n / this boards
+#define SDK_SOLVE4_TAIL_DIV 128       // the shared dequeue tail: n / this boards (32 to round 3: profiles/r03/ab_tail_size2.log)
 #endif
 #ifndef SDK_SOLVE4_TAIL_CHUNK_DIV
 #define SDK_SOLVE4_TAIL_CHUNK_DIV 1   // tail chunks: chunk / this boards
@@ -1622,7 +1622,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         s_dnepoch4 = ld_agent(&a.dn->epoch);
         s_dngrid4 = grid;
     }
-    {   // segments share the first n - n/32 boards (rounded to whole chunks); the rest is the tail
+    {   // segments share the first n - n/128 boards (rounded to whole chunks); the rest is the tail
         a.tail_chunk = max(1u, args.chunk / SDK_SOLVE4_TAIL_CHUNK_DIV);
         const uint64_t tail = ((n / SDK_SOLVE4_TAIL_DIV + args.chunk - 1) / args.chunk) * args.chunk;
         a.tail0 = (uint32_t)(n - min<uint64_t>(tail, n));

@@ -83,7 +83,7 @@ struct SolveArgs {
                                // length, written by an earlier launch); `n` is then its bound
 };
 
-// per-XCD dequeue: the first n - n/32 boards are cut into kHeads contiguous segments with a
+// per-XCD dequeue: the first n - n/128 boards are cut into kHeads contiguous segments with a
 // head each, workgroup g takes chunks of segment g % kHeads (the XCD the round-robin
 // dispatch put it on) and, once that is drained, of the shared tail (one more head);
 // heads kHeadStride words apart (own cache lines)

@@ -54,7 +54,7 @@ __device__ __forceinline__ void expand4_load(const Lane4& w, const ExpandArgs& a
 // classification, branch and propagated board of slot HI (its round ended in an event)
 template <int HI>
 __device__ __forceinline__ void expand4_out(const Lane4& w, const ExpandArgs& a, uint64_t i, bool contra,
-                                            const Cells4& c) {
+                                            const Cells4& c, uint32_t& nleaves, uint32_t& nopen) {
     const uint32_t x0 = fld<HI>(c.x0), x1 = fld<HI>(c.x1), x2 = fld<HI>(c.x2);
     const uint32_t s0 = fld<HI>(c.s0), s1 = fld<HI>(c.s1), s2 = fld<HI>(c.s2);
     uint32_t nch = 0u, cell = 0u, m = 0u;
@@ -66,11 +66,11 @@ __device__ __forceinline__ void expand4_out(const Lane4& w, const ExpandArgs& a,
                 nch = 1u;
                 m = kKeepBoard;
                 write = true;
-            } else if (w.hl == 0) {
-                atomicAdd(&a.ctl->lvl_leaves, 1ull);
+            } else {
+                ++nleaves;
             }
         } else {
-            if (w.hl == 0) atomicAdd(&a.ctl->open, 1ull);
+            ++nopen;
             if (a.order == ORDER_LEX) {
                 int cl;
                 uint32_t mm;
@@ -114,6 +114,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
     const uint64_t m = a.ctl->m;
     Lane4 w;
     init_lane4(w, s_region, s_in);
+    // the level's leaves and branching boards, counted per half and added once per wave at the
+    // end: one same-address atomic per board serialized (~10 ns each) and bound the level
+    uint32_t nleaves = 0u, nopen = 0u;
     for (uint64_t base = (uint64_t)blockIdx.x * 4u; base < m; base += (uint64_t)gridDim.x * 4u) {
         const uint64_t i0 = base + 2u * (uint64_t)w.half, i1 = i0 + 1u;   // this half's slots 0 and 1
         const bool v0 = i0 < m, v1 = i1 < m;
@@ -143,9 +146,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_SOLVE4_W
             act0 &= ~E0;
             act1 &= ~E1;
         }
-        if (v0) expand4_out<0>(w, a, i0, __builtin_amdgcn_inverse_ballot_w64(con0), c);
-        if (v1) expand4_out<1>(w, a, i1, __builtin_amdgcn_inverse_ballot_w64(con1), c);
+        if (v0) expand4_out<0>(w, a, i0, __builtin_amdgcn_inverse_ballot_w64(con0), c, nleaves, nopen);
+        if (v1) expand4_out<1>(w, a, i1, __builtin_amdgcn_inverse_ballot_w64(con1), c, nleaves, nopen);
     }
+    const uint32_t tl = __builtin_amdgcn_readlane(nleaves, 0) + __builtin_amdgcn_readlane(nleaves, 32);
+    const uint32_t to = __builtin_amdgcn_readlane(nopen, 0) + __builtin_amdgcn_readlane(nopen, 32);
+    if (threadIdx.x == 0 && tl) atomicAdd(&a.ctl->lvl_leaves, (unsigned long long)tl);
+    if (threadIdx.x == 0 && to) atomicAdd(&a.ctl->open, (unsigned long long)to);
 }
 #endif
 

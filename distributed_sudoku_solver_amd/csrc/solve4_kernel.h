@@ -653,6 +653,9 @@ static __shared__ uint32_t s_dnwave4; // bit 0: counted in `finished`, bit 1: re
 static __shared__ uint32_t s_dnepoch4;
 static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
 static __shared__ uint32_t s_deq4;     // the wave's dequeue stage (next_board4)
+static __shared__ unsigned long long s_count4;   // count mode: the wave's completions (added to
+                                                 // *count once, at the end: same-address atomics
+                                                 // per board serialize at ~10 ns)
 
 // runtime-slot field access (the donation paths run once per loop iteration for any slot)
 __device__ __forceinline__ uint32_t fld_rt(uint32_t w, uint32_t hi) {
@@ -1313,7 +1316,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
     if (DN && a.order != ORDER_LEX && st == -2) st = kDnRetryLex;
     uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
     if (a.count_mode && w.hl == 0 && st != -2 && b.count)
-        atomicAdd(a.count, (unsigned long long)b.count);
+        atomicAdd(&s_count4, (unsigned long long)b.count);
     if (st != 1 && w.act && a.out) {  // the reference restores the grid (DHT_Node.py:535)
         const uint8_t* sin = w.s_in + HI * 81;
         dst[w.c0] = sin[w.c0];
@@ -1448,7 +1451,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
         }
         if (b.count >= b.lim && a.count_mode && !a.count_stop) {
             // 2^31 completions on one board: move all but one to the total and go on
-            if (w.hl == 0) atomicAdd(a.count, (unsigned long long)(b.count - 1u));
+            if (w.hl == 0) atomicAdd(&s_count4, (unsigned long long)(b.count - 1u));
             b.count = 1;
         } else if (b.count >= b.lim) {
             if (b.order == ORDER_MRV && !a.count_mode) {      // >= 2 completions: lex re-search
@@ -1587,7 +1590,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     __shared__ Slot4 s_slot[4];
     Lane4 w;
     init_lane4(w, s_region, s_in);
-    if (threadIdx.x == 0) s_deq4 = 0u;
+    if (threadIdx.x == 0) {
+        s_deq4 = 0u;
+        s_count4 = 0ull;
+    }
 #if SDK_SOLVE4_PROFILE
     if (threadIdx.x < 10) s_prof4[threadIdx.x] = 0;
     __syncthreads();
@@ -1698,6 +1704,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
                 if (threadIdx.x == 0) s_dnpend4 = 0u;
             }
         }
+    }
+    if (a.count_mode && threadIdx.x == 0) {
+        const unsigned long long n = s_count4;
+        if (n) atomicAdd(a.count, n);
     }
 #if SDK_SOLVE4_PROFILE
     prof4_add(8, __builtin_amdgcn_s_memtime() - tl_);

@@ -341,6 +341,14 @@ def default_target(engine, world):
     return engine.get_option(L.SDK_OPT_DEVICE_CUS) * engine.get_option(L.SDK_OPT_WAVES_PER_CU) * 8 * world
 
 
+def count_target(engine, world):
+    """Frontier size of an exhaustive count: 64 boards per resident solver wave per GPU (512k on
+    an MI355X).  A count launch ends with its heaviest subtrees, so finer subtrees shorten it,
+    and the frontier build is cheap (1M boards in 1.7 ms): 14-clue C5 board 46.9 ms at 65k boards,
+    24.3 ms at 512k, 22.8 ms at 1M; 15-clue 7.1 / 6.0 / 6.2 ms (profiles/r03/c5_target.log)."""
+    return default_target(engine, world) * 8
+
+
 def sharded_count(engine, board, rank, world, limit=0, comm=None, target=None, refine=True):
     """Count the completions of `board` with `world` ranks (one GPU each).
 
@@ -358,12 +366,12 @@ def sharded_count(engine, board, rank, world, limit=0, comm=None, target=None, r
     two_stage = world > 1 and refine and hasattr(engine, "frontier_refine")
     if two_stage:
         size, leaves0 = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT, target=1024 * world)
-        mine, leaves1 = engine.frontier_refine(rank, world, default_target(engine, 1) if target is None else target)
+        mine, leaves1 = engine.frontier_refine(rank, world, count_target(engine, 1) if target is None else target)
         first, step, end = 0, 1, mine
         own_leaves = leaves1 + (leaves0 if rank == 0 else 0)
     else:
         size, leaves = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT,
-                                             target=default_target(engine, world) if target is None else target)
+                                             target=count_target(engine, world) if target is None else target)
         first, step, end = rank, world, size
         own_leaves = None
     res = engine.result_buffer(2, np.uint64)
@@ -478,7 +486,7 @@ def sharded_count_rebalanced(engine, board, rank, world, limit=0, comm=None, tar
     if world > 1 and comm is None:
         raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
     size, leaves = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT,
-                                         target=default_target(engine, world) if target is None else target)
+                                         target=count_target(engine, world) if target is None else target)
     if chunk is None:   # one launch when there is no one to rebalance with; else 2 boards per resident wave
         chunk = max(1, size) if comm is None else max(1, default_target(engine, 1) // 4)
     lo, hi = shard_bounds(size, rank, world) if ranges is None else (int(ranges[rank][0]), int(ranges[rank][1]))

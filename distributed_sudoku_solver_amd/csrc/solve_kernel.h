@@ -92,6 +92,10 @@ struct SolveArgs {
 #endif
 constexpr int kHeads = SDK_HEADS;   // a multiple of 8: segment g % kHeads stays on one XCD
 constexpr int kHeadStride = 64;
+// the heads buffer: kHeads segment heads, the shared tail, then the launch's dequeue counter, so
+// one memset clears a QUAD launch's dequeue state
+constexpr int kHeadNext = (kHeads + 1) * kHeadStride;
+constexpr int kHeadWords = (kHeads + 2) * kHeadStride;
 
 __device__ __forceinline__ uint32_t cell_init(uint32_t v) {
     return v == 0 ? kCands : (v <= 9 ? ((1u << (v - 1)) | kClue) : kInert);

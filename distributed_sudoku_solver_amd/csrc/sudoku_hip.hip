@@ -304,8 +304,15 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     if (rc) return rc;
     rc = ensure(c->counter, 256);
     if (rc) return rc;
-    if (dn_phase == 0)   // word 0 = work counter; words 1.. belong to callers
+    // QUAD with per-XCD heads: the dequeue counter lives in the heads buffer (one memset per
+    // launch clears both); otherwise word 0 of c->counter (words 1.. belong to callers)
+    const bool use_heads = four && c->xcd_heads && dn_phase != 2;
+    if (use_heads) {
+        if ((rc = ensure(c->heads, sdk::kHeadWords * sizeof(uint32_t)))) return rc;
+        if (dn_phase == 0) HIPCALL(hipMemsetAsync(c->heads.p, 0, sdk::kHeadWords * sizeof(uint32_t), c->stream));
+    } else if (dn_phase == 0) {
         HIPCALL(hipMemsetAsync(c->counter.p, 0, 8, c->stream));
+    }
     sdk::SolveArgs a;
     a.in = d_in;
     a.mask = d_mask;
@@ -313,7 +320,7 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     a.status = d_status;
     a.work = d_work;
     a.n = n;
-    a.next = static_cast<uint32_t*>(c->counter.p);
+    a.next = use_heads ? static_cast<uint32_t*>(c->heads.p) + sdk::kHeadNext : static_cast<uint32_t*>(c->counter.p);
     a.stack = static_cast<uint32_t*>(c->stack.p);
     a.budget = node_budget;
     a.order = order >= 0 ? order : c->order;
@@ -354,13 +361,7 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
             a.stack = static_cast<uint32_t*>(c->stack.p);
         }
     }
-    if (four && c->xcd_heads && dn_phase != 2) {
-        rc = ensure(c->heads, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t));
-        if (rc) return rc;
-        if (dn_phase == 0)
-            HIPCALL(hipMemsetAsync(c->heads.p, 0, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t), c->stream));
-        a.heads = static_cast<uint32_t*>(c->heads.p);
-    }
+    if (use_heads) a.heads = static_cast<uint32_t*>(c->heads.p);
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
     if (rc) return rc;
@@ -453,13 +454,13 @@ int dn_prep(sdk_ctx* c, uint64_t cap, bool first_pass) {
         c->dn_epoch = 0;
     }
     if ((rc = ensure(c->dn_stat, 256)) || (rc = ensure(c->counter, 256)) ||
-        (rc = ensure(c->heads, (sdk::kHeads + 1) * sdk::kHeadStride * sizeof(uint32_t))) ||
+        (rc = ensure(c->heads, sdk::kHeadWords * sizeof(uint32_t))) ||
         (rc = ensure(c->dn_list, (cap + 1) * sizeof(uint32_t))) || (rc = ensure(c->dn3_list, (cap + 1) * sizeof(uint32_t))))
         return rc;
     sdk::DnPrep p{};
     p.counter = static_cast<uint32_t*>(c->counter.p);
     p.heads = c->xcd_heads ? static_cast<uint32_t*>(c->heads.p) : nullptr;
-    p.heads_words = (sdk::kHeads + 1) * sdk::kHeadStride;
+    p.heads_words = sdk::kHeadWords;   // the heads and the dequeue counter after them
     p.stat = first_pass ? static_cast<uint32_t*>(c->dn_stat.p) : nullptr;   // statistics add up over passes
     for (int k = 0; k < 2; ++k) {
         p.ctl[k] = reinterpret_cast<uint32_t*>(static_cast<char*>(c->dn.p) + (size_t)k * sdk::kDnBytes);

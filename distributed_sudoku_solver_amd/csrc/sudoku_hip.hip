@@ -144,6 +144,7 @@ struct sdk_ctx {
                                   // grid only adds waves that start once the queue is drained: 1 % slower, r02)
     // workspaces
     DevBuf stack, counter, heads, in, mask, out, status, work, verdict;
+    uint32_t heads_round = 0;      // launches since the heads pool was cleared (kHeadRounds regions)
     int xcd_heads = 1;             // QUAD: per-XCD dequeue heads (SDK_OPT_XCD_HEADS)
     int donate = 1;                // QUAD, LEX solves: subtree donation (SDK_OPT_DONATE)
     DevBuf dn;                     // two donation areas (solve4_kernel.h: DnCtl, records, items,
@@ -178,6 +179,7 @@ struct sdk_ctx {
 namespace {
 
 constexpr uint64_t kDnSplitDefault = 256;   // SDK_OPT_DONATE = 1: split budget (search nodes) of the plain phase
+constexpr uint32_t kHeadRounds = 64;        // dequeue-head regions per clear (launch_solve_once)
 
 int ensure(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes) return SDK_OK;
@@ -304,12 +306,22 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     if (rc) return rc;
     rc = ensure(c->counter, 256);
     if (rc) return rc;
-    // QUAD with per-XCD heads: the dequeue counter lives in the heads buffer (one memset per
-    // launch clears both); otherwise word 0 of c->counter (words 1.. belong to callers)
+    // QUAD with per-XCD heads: the dequeue counter lives in the heads region after the heads.
+    // Plain launches take a fresh region of a pool of kHeadRounds, cleared by one memset every
+    // kHeadRounds launches (a per-launch memset is its own ~4 us dispatch in front of the
+    // kernel); the split phase's region is cleared by its prep launch.  Otherwise the counter
+    // is word 0 of c->counter (words 1.. belong to callers).
     const bool use_heads = four && c->xcd_heads && dn_phase != 2;
+    uint32_t* heads = nullptr;
     if (use_heads) {
-        if ((rc = ensure(c->heads, sdk::kHeadWords * sizeof(uint32_t)))) return rc;
-        if (dn_phase == 0) HIPCALL(hipMemsetAsync(c->heads.p, 0, sdk::kHeadWords * sizeof(uint32_t), c->stream));
+        if ((rc = ensure(c->heads, (size_t)kHeadRounds * sdk::kHeadWords * sizeof(uint32_t)))) return rc;
+        uint32_t region = 0;
+        if (dn_phase == 0) {
+            region = c->heads_round++ % kHeadRounds;
+            if (region == 0)
+                HIPCALL(hipMemsetAsync(c->heads.p, 0, (size_t)kHeadRounds * sdk::kHeadWords * sizeof(uint32_t), c->stream));
+        }
+        heads = static_cast<uint32_t*>(c->heads.p) + (size_t)region * sdk::kHeadWords;
     } else if (dn_phase == 0) {
         HIPCALL(hipMemsetAsync(c->counter.p, 0, 8, c->stream));
     }
@@ -320,7 +332,7 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     a.status = d_status;
     a.work = d_work;
     a.n = n;
-    a.next = use_heads ? static_cast<uint32_t*>(c->heads.p) + sdk::kHeadNext : static_cast<uint32_t*>(c->counter.p);
+    a.next = use_heads ? heads + sdk::kHeadNext : static_cast<uint32_t*>(c->counter.p);
     a.stack = static_cast<uint32_t*>(c->stack.p);
     a.budget = node_budget;
     a.order = order >= 0 ? order : c->order;
@@ -361,7 +373,7 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
             a.stack = static_cast<uint32_t*>(c->stack.p);
         }
     }
-    if (use_heads) a.heads = static_cast<uint32_t*>(c->heads.p);
+    if (use_heads) a.heads = heads;
     hipEvent_t stop;
     rc = timer_begin(c, &stop);
     if (rc) return rc;
@@ -454,7 +466,7 @@ int dn_prep(sdk_ctx* c, uint64_t cap, bool first_pass) {
         c->dn_epoch = 0;
     }
     if ((rc = ensure(c->dn_stat, 256)) || (rc = ensure(c->counter, 256)) ||
-        (rc = ensure(c->heads, sdk::kHeadWords * sizeof(uint32_t))) ||
+        (rc = ensure(c->heads, (size_t)kHeadRounds * sdk::kHeadWords * sizeof(uint32_t))) ||
         (rc = ensure(c->dn_list, (cap + 1) * sizeof(uint32_t))) || (rc = ensure(c->dn3_list, (cap + 1) * sizeof(uint32_t))))
         return rc;
     sdk::DnPrep p{};

@@ -446,7 +446,7 @@ def hard_leg(eng, d, args, synth, L):
             el, b = _timed_solves(eng, d, bp, bs, 5)
             bad += b
             legs[mode] = {"value": d.world * len(bp) / el, "unit": "puzzles/s", "ms": el * 1000.0,
-                          "split_budget": dn if dn > 1 else (256 if dn else None),
+                          "split_budget": dn if dn > 1 else (128 if dn else None),
                           "split_boards": eng.get_option(L.SDK_OPT_SPLIT_BOARDS),
                           "lex_boards": eng.get_option(L.SDK_OPT_LEX_BOARDS),
                           "donated": eng.get_option(L.SDK_OPT_DONATED)}

@@ -178,7 +178,8 @@ struct sdk_ctx {
 
 namespace {
 
-constexpr uint64_t kDnSplitDefault = 256;   // SDK_OPT_DONATE = 1: split budget (search nodes) of the plain phase
+constexpr uint64_t kDnSplitDefault = 128;   // SDK_OPT_DONATE = 1: split budget (search nodes) of the plain phase
+                                            // (256 to round 3; profiles/r03/sweep_split_r03.log)
 constexpr uint32_t kHeadRounds = 64;        // dequeue-head regions per clear (launch_solve_once)
 
 int ensure(DevBuf& b, size_t bytes) {

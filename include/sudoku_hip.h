@@ -84,7 +84,7 @@ extern "C" {
 #define SDK_OPT_DONATE       15  /* QUAD solver, SDK_ORDER_LEX solves: two-phase solve   */
                                  /* with subtree donation.  1 (default) or a split       */
                                  /* budget >= 2: every board first gets at most that     */
-                                 /* many search nodes (1: 256); the boards that need     */
+                                 /* many search nodes (1: 128); the boards that need     */
                                  /* more are solved again by the donation kernel, where  */
                                  /* idle waves take a heavy board's shallowest untried   */
                                  /* branches.  Same boards and statuses; `work` adds up  */

@@ -11,6 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SDK_LIB_PATH", os.path.join(HERE, "libsudoku_hip.so"))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "sudoku_hip.h")
 
+SDK_ABI_VERSION = 2
 SDK_OK = 0
 SDK_EINVAL = -1
 SDK_EHIP = -2
@@ -45,6 +46,8 @@ SDK_OPT_SPLIT_BOARDS = 17
 SDK_OPT_DONATE_MODE = 18
 SDK_OPT_LEX_BOARDS = 19
 SDK_OPT_DONATE_MAX = 20
+SDK_OPT_DN_FAULT = 21
+SDK_DONATE_CONTEXT = -1    # sdk_solve_batch_ex: use the context's SDK_OPT_DONATE
 SDK_CHECK_REG1 = 0
 SDK_CHECK_REG2 = 1
 SDK_CHECK_GLDS2 = 2
@@ -73,6 +76,8 @@ SDK_COMM_U8 = 2
 SDK_COMM_SUM = 0
 SDK_COMM_MIN = 1
 SDK_COMM_MAX = 2
+SDK_COMM_SEND = 0
+SDK_COMM_RECV = 1
 
 # every symbol the header declares: name -> (restype, argtypes)
 _vp = ctypes.c_void_p
@@ -89,6 +94,14 @@ SIGNATURES = {
     "sdk_check_batch_i64": (ctypes.c_int, [_vp, _vp, _vp, _sz]),
     "sdk_solve_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz]),
     "sdk_solve_batch_budget": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint64]),
+    "sdk_solve_batch_ex": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint64, ctypes.c_int64]),
+    "sdk_frontier_boards_dev": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64)]),
+    "sdk_frontier_load_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64]),
+    "sdk_frontier_refine_range": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "sdk_comm_send_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int]),
+    "sdk_comm_recv_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int]),
+    "sdk_comm_p2p_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _vp]),
     "sdk_expand_boards": (ctypes.c_int, [_vp, _vp, _vp, _sz, ctypes.c_uint64, _vp, _sz,
                                          ctypes.POINTER(ctypes.c_uint64)]),
     "sdk_count_solutions": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),

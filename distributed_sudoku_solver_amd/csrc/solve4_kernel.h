@@ -547,22 +547,28 @@ struct Args4 : Args2 {
 // input (total 0), or marks the board kDnRetryLex (several completions, or a part that
 // hit the node budget) for a LEX donation launch.
 //
-// Hand-off without a shared queue word: a wave whose four slots are idle counts itself
-// in `finished`, registers its id once (reg[reg_tail++]) and polls only its own mailbox.
-// A donor takes registrations (reg_head += k, at most as many as are registered), takes
-// each receiver out of `finished` and stores the item index in its mailbox.  A wave leaves
-// when every wave of the grid is counted idle: no part is running, so no item can be on
-// its way (receivers are un-counted by their donor before the delivery).  Registrations a
-// donor reserved but could not use are simply never served.  The counters and registries
-// are kept per XCD (workgroup % 8, the dispatch's round robin), each on its own cache
-// line: thousands of waves go idle at once when the launch starts or drains, and one
-// shared counter would serialise their atomics; a donor serves its own XCD's idle waves
-// first (the item it writes is then in that XCD's L2).
+// Hand-off without a shared queue word: a wave counts itself busy when it starts (before
+// its first dequeue); once its four slots are idle it un-counts itself, registers its id
+// once (reg[reg_tail++]) and polls only its own mailbox.  A donor takes registrations
+// (reg_head moves by compare-and-swap, never past reg_tail), counts each receiver busy
+// again and only then stores the item index in its mailbox, and adds the items to
+// `delivered`.  A wave leaves when no wave is counted busy: no part is running, and no
+// item can be on its way.  Only waves that started are ever counted, so the launch ends
+// whether or not its whole grid was resident at once (a GPU shared with another kernel
+// dispatches the rest of the grid later; those waves find nothing and leave).  The sum of
+// the per-XCD counters is not one snapshot, so the check reads `delivered` before and
+// after it and leaves only if no delivery happened in between (a delivery precedes the
+// donor's own idle decrement).  Every wait on another wave is bounded in time
+// (kDnWaitTicks); one that runs out sets `err` (the host fails the solve with SDK_EHIP)
+// and stops all further donation.  The counters and registries are kept per XCD
+// (workgroup % 8, the dispatch's round robin), each on its own cache line: thousands of
+// waves start and go idle at once, and one shared counter would serialise their atomics;
+// a donor serves its own XCD's idle waves first (the item it writes is then in that XCD's L2).
 constexpr int kDnXcds = 8;
 struct DnXcd {
-    uint32_t finished;        // waves of this XCD counted idle
+    uint32_t busy;            // waves of this XCD counted working (entry +1, idle -1, delivery +1)
     uint32_t reg_tail;        // registrations of idle waves
-    uint32_t reg_head;        // registrations taken by donors
+    uint32_t reg_head;        // registrations taken by donors (<= reg_tail)
     uint32_t pad[29];
 };
 struct DnCtl {
@@ -573,9 +579,18 @@ struct DnCtl {
     uint32_t nrec;            // board records handed out
     uint32_t exit_all, parts_ended, finalized;   // diagnostics
     uint32_t next;            // the launch's board dequeue counter
-    uint32_t pad[24];
+    uint32_t err;             // sticky (not cleared by the prep launch; the host reads and clears
+                              // it): kDnErrReg / kDnErrLock, a bounded wait ran out
+    uint32_t fault;           // test only (SDK_OPT_DN_FAULT): registrations are not written
+    uint32_t started;         // diagnostics: waves that took part
+    uint32_t pad[21];
     DnXcd x[kDnXcds];
 };
+constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u;
+// bound of every wait on another wave, in s_memrealtime ticks (100 MHz): 0.2 s -- a
+// registration is written right after its ticket is drawn and a lock is held for a few
+// hundred cycles, so only a wave that cannot run (a fault, or a preempted queue) gets near it
+constexpr uint64_t kDnWaitTicks = 20000000ull;
 constexpr uint32_t kDnItems = 1u << 16;
 constexpr uint32_t kDnRecs = 1u << 14;
 constexpr uint32_t kDnRegX = 1u << 14;        // registrations per XCD
@@ -649,7 +664,7 @@ struct DnFin {
 static __shared__ SlotDn s_dn4[4];    // per slot (half * 2 + slot); referenced by solve4_kernel<true> only
 static __shared__ DnFin s_dnfin4[4];
 static __shared__ uint32_t s_dnpend4; // bit k: s_dnfin4[k] waits; bit 4 + k: slot k's check is due
-static __shared__ uint32_t s_dnwave4; // bit 0: counted in `finished`, bit 1: registered, bits 8..: polls
+static __shared__ uint32_t s_dnwave4; // bit 0: un-counted from `busy` (idle), bit 1: registered, bits 8..: polls
 static __shared__ uint32_t s_dnepoch4;
 static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
 static __shared__ uint32_t s_deq4;     // the wave's dequeue stage (next_board4)
@@ -759,6 +774,7 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     }
     if (x == kDnXcds) return;                                     // no idle wave waits
     if (half_any4(w, w.act && fld_rt(c.E, hi) == 0u)) return;   // only boards with every unit exact
+    if (ld_agent(&ctl->err) != 0u) return;                        // a bounded wait ran out: no more donation
     const uint32_t lvl = d.base;
     uint2* lp = g_stk + (lvl * 2 + hi) * 64 + w.lane;
     const uint2 snap = *lp;
@@ -766,13 +782,24 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     const int cell = (int)(rec16 & 0x7Fu);
     const uint32_t rest = rec16 >> 7;
     const uint32_t cnt = (uint32_t)__popc(rest);
-    // registrations: tickets t0 .. t0 + valid - 1 are registered idle waves
+    // registrations: tickets t0 .. t0 + valid - 1 are registered idle waves.  reg_head moves
+    // by compare-and-swap and never past a reg_tail value read before, so every ticket a
+    // donor takes belongs to a wave that registered (a plain add with a stale head could
+    // pass reg_tail and leave later registrations below it, never served)
     uint32_t t0 = 0, valid = 0;
-    if (w.hl == 0) {
-        const uint32_t want = min(cnt, tail - head);
-        t0 = atomicAdd(&ctl->x[x].reg_head, want);
-        const uint32_t tail2 = min(ld_agent(&ctl->x[x].reg_tail), kDnRegX);
-        valid = tail2 > t0 ? min(want, tail2 - t0) : 0u;
+    if (w.hl == 0 && cnt != 0u) {
+        uint32_t h = head, t = min(tail, kDnRegX);
+        for (int it = 0; it < 8 && t > h; ++it) {
+            const uint32_t want = min(cnt, t - h);
+            const uint32_t old = atomicCAS(&ctl->x[x].reg_head, h, h + want);
+            if (old == h) {
+                t0 = h;
+                valid = want;
+                break;
+            }
+            h = old;
+            t = min(ld_agent(&ctl->x[x].reg_tail), kDnRegX);
+        }
     }
     t0 = half_first4(w, t0);
     valid = half_first4(w, valid);
@@ -838,9 +865,22 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
         unsigned long long* reg = dn_reg4(a) + (size_t)x * kDnRegX;
         unsigned long long* mbox = dn_mbox4(a);
         for (uint32_t k = 0; k < valid; ++k) {
+            // the registrant writes its entry right after drawing the ticket: a bounded wait
             unsigned long long e;
-            while (((e = ld_agent64(reg + t0 + k)) >> 32) != epoch) __builtin_amdgcn_s_sleep(1);
-            atomicSub(&ctl->x[x].finished, 1u);                     // the receiver works from now on
+            const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+            bool ok = true;
+            while (((e = ld_agent64(reg + t0 + k)) >> 32) != epoch) {
+                if (__builtin_amdgcn_s_memrealtime() - t_start > kDnWaitTicks) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!ok) {   // the items left stay undelivered: the solve reports SDK_EHIP
+                atomicOr(&ctl->err, kDnErrReg);
+                break;
+            }
+            atomicAdd(&ctl->x[x].busy, 1u);                         // the receiver works from now on
             __hip_atomic_store(mbox + (uint32_t)e, ((unsigned long long)epoch << 32) | (i0 + k), __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -910,8 +950,18 @@ __device__ __forceinline__ void dn_finish_part4(const Lane4& w, const Args4& a, 
         // fold the part's completion into the board's running minimum.  Only this half of the
         // wave runs here (the caller's loop takes one slot at a time), so the spinning lane
         // never waits on its own wave; other waves' holders finish without it.
-        if (w.hl == 0)
-            while (atomicExch(&r->lock, 1u) != 0u) __builtin_amdgcn_s_sleep(1);   // test-and-set
+        // test-and-set, bounded: a holder that cannot finish sets `err` (the fold goes on
+        // unlocked; the solve then reports SDK_EHIP and its boards are not used)
+        if (w.hl == 0) {
+            const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+            while (atomicExch(&r->lock, 1u) != 0u) {
+                if (__builtin_amdgcn_s_memrealtime() - t_start > kDnWaitTicks) {
+                    atomicOr(&a.dn->err, kDnErrLock);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         const bool had = ld_agent(&r->have) != 0u;
         uint32_t s0, s1, s2, b0, b1, b2;
@@ -1025,13 +1075,16 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(s_dnepoch4);
     unsigned long long* mbox = dn_mbox4(a) + blockIdx.x;
     if (!(st & 1u)) {
-        if (w.lane == 0) atomicAdd(&mx->finished, 1u);
+        // this wave's deliveries (`delivered`) before its idle count: an exit check that sees
+        // the decrement sees them (see the hand-off above)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (w.lane == 0) atomicSub(&mx->busy, 1u);
         st |= 1u;
     }
     if (!(st & 2u)) {
         if (w.lane == 0) {
             const uint32_t t = atomicAdd(&mx->reg_tail, 1u);
-            if (t < kDnRegX)
+            if (t < kDnRegX && ld_agent(&ctl->fault) == 0u)
                 __hip_atomic_store(dn_reg4(a) + (size_t)(blockIdx.x % kDnXcds) * kDnRegX + t,
                                    ((unsigned long long)epoch << 32) | blockIdx.x, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -1044,7 +1097,7 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
     const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
     if (mhi == epoch) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the item's words
-        // delivered: the donor took this wave out of `finished`; its registration is spent
+        // delivered: the donor counted this wave busy again; its registration is spent
         const uint32_t idx = __builtin_amdgcn_readfirstlane((uint32_t)m);
         if (w.lane == 0) __hip_atomic_store(mbox, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (w.lane == 0) s_dnwave4 = 0u;
@@ -1052,13 +1105,19 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
         A0 = 0x00000000FFFFFFFFull;
         return 2;
     }
-    st += 0x100u;                             // polls; the grid-wide idle count every 16th
+    st += 0x100u;                             // polls; the grid-wide busy count every 16th
     if (w.lane == 0) s_dnwave4 = st;
     if (((st >> 8) & 15u) == 1u) {
-        uint32_t fin = 0;
-        for (int k = 0; k < kDnXcds; ++k) fin += ld_agent(&ctl->x[k].finished);
-        fin = __builtin_amdgcn_readfirstlane(fin);
-        if (fin >= __builtin_amdgcn_readfirstlane(s_dngrid4)) {
+        // leave when no started wave is busy and no delivery happened while the eight
+        // counters were read (they are not one snapshot: see the hand-off above)
+        const uint32_t v1 = ld_agent(&ctl->delivered);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        uint32_t busy = 0;
+        for (int k = 0; k < kDnXcds; ++k) busy += ld_agent(&ctl->x[k].busy);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t v2 = ld_agent(&ctl->delivered);
+        busy = __builtin_amdgcn_readfirstlane(busy);
+        if (busy == 0u && __builtin_amdgcn_readfirstlane(v1) == __builtin_amdgcn_readfirstlane(v2)) {
             if (w.lane == 0) atomicAdd(&ctl->exit_all, 1u);
             return 0;
         }
@@ -1577,6 +1636,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     // device (the list the previous phase left), and the launch is the full resident grid, of
     // which 64 + 16 waves per board take part (a few tail boards do not need thousands of
     // idle waves registering and polling; none when nothing was listed)
+    // dn_donate4 reads and rewrites a donated level in the global stack
+    static_assert(!DN || kLds4Levels == 0, "subtree donation needs every DFS level in the global stack");
     uint64_t n = args.n;
     uint32_t grid = gridDim.x;
     if constexpr (DN) {
@@ -1627,6 +1688,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         s_dnwave4 = 0u;
         s_dnepoch4 = ld_agent(&a.dn->epoch);
         s_dngrid4 = grid;
+        // counted busy before the first dequeue (release): a wave whose dequeue comes up empty
+        // after this one's took a board sees this count (see the hand-off above)
+        atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u);
+        atomicAdd(&a.dn->started, 1u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
     {   // segments share the first n - n/128 boards (rounded to whole chunks); the rest is the tail
         a.tail_chunk = max(1u, args.chunk / SDK_SOLVE4_TAIL_CHUNK_DIV);

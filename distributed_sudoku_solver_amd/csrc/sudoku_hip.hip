@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -95,6 +96,7 @@ struct DnPrep {
     uint32_t* stat;
     uint32_t* ctl[2];
     uint32_t epoch[2];
+    uint32_t fault;      // DnCtl.fault (SDK_OPT_DN_FAULT, test only)
     uint32_t* list[2];
 };
 __global__ void dn_prep_kernel(DnPrep p) {
@@ -107,8 +109,12 @@ __global__ void dn_prep_kernel(DnPrep p) {
     if (p.stat && t < 2) p.stat[t] = 0;
     if (p.heads)
         for (uint32_t i = t; i < p.heads_words; i += blockDim.x) p.heads[i] = 0;
+    // every word but the sticky error word (the host reads and clears it after the solve)
+    constexpr uint32_t kEpoch = offsetof(DnCtl, epoch) / 4, kErr = offsetof(DnCtl, err) / 4,
+                       kFault = offsetof(DnCtl, fault) / 4;
     for (int k = 0; k < 2; ++k)
-        for (uint32_t i = t; i < sizeof(DnCtl) / 4; i += blockDim.x) p.ctl[k][i] = i == 0 ? p.epoch[k] : 0u;
+        for (uint32_t i = t; i < sizeof(DnCtl) / 4; i += blockDim.x)
+            if (i != kErr) p.ctl[k][i] = i == kEpoch ? p.epoch[k] : (i == kFault ? p.fault : 0u);
 }
 __global__ void dn_scatter_kernel(const uint32_t* list, const uint8_t* sub_out, const int8_t* sub_st,
                                   const uint64_t* sub_work, bool depth, uint8_t* out, int8_t* status, uint64_t* work) {
@@ -156,6 +162,8 @@ struct sdk_ctx {
                                    // kernel, [1] of those, boards re-solved in LEX order
     bool dn_ran = false;           // the last solve was phased (dn_stat and `delivered` are its)
     bool timer_hold = false;       // a phased solve is being timed as one span
+    bool dn_err_check = false;     // a phased solve ran since its control blocks' error words were read
+    int dn_fault = 0;              // SDK_OPT_DN_FAULT (test only)
     int dn_exhaustive = 1;         // phase 2 in MRV count-to-2 order (SDK_OPT_DONATE_MODE)
     int64_t dn_max = 1 << 19;      // largest batch solved in phases (SDK_OPT_DONATE_MAX, 0 = any)
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
@@ -479,6 +487,7 @@ int dn_prep(sdk_ctx* c, uint64_t cap, bool first_pass) {
         p.ctl[k] = reinterpret_cast<uint32_t*>(static_cast<char*>(c->dn.p) + (size_t)k * sdk::kDnBytes);
         p.epoch[k] = ++c->dn_epoch;
     }
+    p.fault = c->dn_fault ? 1u : 0u;
     p.list[0] = static_cast<uint32_t*>(c->dn_list.p);
     p.list[1] = static_cast<uint32_t*>(c->dn3_list.p);
     sdk::dn_prep_kernel<<<1, 256, 0, c->stream>>>(p);
@@ -489,14 +498,17 @@ int dn_prep(sdk_ctx* c, uint64_t cap, bool first_pass) {
 int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
                  uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
                  unsigned long long* d_counts = nullptr, uint64_t in_first = 0, uint64_t in_step = 1,
-                 int order = -1, int64_t budget = -1) {
+                 int order = -1, int64_t budget = -1, int64_t donate = -1) {
+    // donate: SDK_OPT_DONATE for this call (-1 = the context's)
     const int eff_order = order >= 0 ? order : c->order;
     const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
-    const uint64_t split = c->donate == 1 ? kDnSplitDefault : (uint64_t)c->donate;
-    const bool two_phase = n > 0 && !count_mode && c->donate && c->solver == SDK_SOLVER_QUAD &&
+    const int64_t dn = donate >= 0 ? donate : (int64_t)c->donate;
+    const uint64_t split = dn == 1 ? kDnSplitDefault : (uint64_t)dn;
+    const bool two_phase = n > 0 && !count_mode && dn && c->solver == SDK_SOLVER_QUAD &&
                            eff_order == SDK_ORDER_LEX && d_out && d_status && (node_budget == 0 || node_budget > split) &&
                            (c->dn_max == 0 || (int64_t)n <= c->dn_max);
     c->dn_ran = two_phase;
+    if (two_phase) c->dn_err_check = true;
     if (!two_phase)
         return launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, count_mode, limit, d_count, d_counts,
                                  in_first, in_step, order, budget, 0);
@@ -632,14 +644,16 @@ int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, i
     return run_frontier_levels(c, 1, h_mask != nullptr, mode, target, h_mask != nullptr);
 }
 
-// Keep frontier boards first, first+step, ... of the current (count-mode) frontier and
+// Keep frontier boards first, first+step, ... < end of the current (count-mode) frontier and
 // expand them further, on this device alone, until they number `target`: the second,
 // rank-local stage of a frontier split, so a rank's share of a replicated frontier can be
-// small and cheap to build.  The leaves reported are those met during this refinement.
-int refine_frontier(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t target) {
+// small and cheap to build; with step 1 and a short range, a rank's last heavy subtrees
+// split into second-level records for the rebalanced count.  The leaves reported are those
+// met during this refinement.
+int refine_frontier(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t end, uint64_t target) {
     if (!c->fr_valid) return fail(SDK_EINVAL, "no frontier: call sdk_frontier_build first");
     if (step == 0) return fail(SDK_EINVAL, "step must be >= 1");
-    const uint64_t m = c->fr_size;
+    const uint64_t m = std::min(end, c->fr_size);
     const uint64_t n = first < m ? (m - first + step - 1) / step : 0;
     c->fr_valid = false;
     target = std::max<uint64_t>(target, n);
@@ -883,6 +897,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 0) return fail(SDK_EINVAL, "SDK_OPT_DONATE_MAX must be >= 0");
             c->dn_max = value;
             return SDK_OK;
+        case SDK_OPT_DN_FAULT:
+            if (value != 0 && value != 1) return fail(SDK_EINVAL, "SDK_OPT_DN_FAULT must be 0 or 1");
+            c->dn_fault = (int)value;
+            return SDK_OK;
         case SDK_OPT_DONATE_MODE:
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "donate mode must be 0 (LEX) or 1 (exhaustive)");
             c->dn_exhaustive = (int)value;
@@ -928,6 +946,28 @@ int read_dn_stat(sdk_ctx* c, int k, int64_t* value) {
     *value = v;
     return SDK_OK;
 }
+
+// The sticky error words of the two donation areas (a bounded wait on another wave inside a
+// donation launch ran out, solve4_kernel.h kDnWaitTicks): read once after a phased solve,
+// cleared, and turned into SDK_EHIP -- the solve's boards are then not valid.
+int dn_check_error(sdk_ctx* c) {
+    if (!c->dn_err_check || !c->dn.p) return SDK_OK;
+    c->dn_err_check = false;
+    uint32_t e[2] = {0u, 0u};
+    for (int k = 0; k < 2; ++k)
+        HIPCALL(hipMemcpyAsync(&e[k], static_cast<char*>(c->dn.p) + (size_t)k * sdk::kDnBytes + offsetof(sdk::DnCtl, err),
+                               sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    const uint32_t err = e[0] | e[1];
+    if (err == 0u) return SDK_OK;
+    for (int k = 0; k < 2; ++k)
+        HIPCALL(hipMemsetAsync(static_cast<char*>(c->dn.p) + (size_t)k * sdk::kDnBytes + offsetof(sdk::DnCtl, err), 0,
+                               sizeof(uint32_t), c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    return fail(SDK_EHIP, "donation launch: a bounded wait on another wave ran out (%s%s); the solve's boards are "
+                "not valid", (err & sdk::kDnErrReg) ? "registration entry never written " : "",
+                (err & sdk::kDnErrLock) ? "record lock never released" : "");
+}
 }  // namespace
 
 int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
@@ -952,6 +992,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_DONATE_MODE: *value = c->dn_exhaustive; return SDK_OK;
         case SDK_OPT_LEX_BOARDS: return read_dn_stat(c, 1, value);
         case SDK_OPT_DONATE_MAX: *value = c->dn_max; return SDK_OK;
+        case SDK_OPT_DN_FAULT: *value = c->dn_fault; return SDK_OK;
         case SDK_OPT_DONATED: {
             // items handed out by the last phased solve's donation launches (of its last
             // kDnCapBoards-board pass; waits for it on the context's stream)
@@ -1003,7 +1044,7 @@ int sdk_memcpy_d2h(sdk_ctx* c, void* dst, const void* src, size_t bytes) {
     HIPCALL(hipSetDevice(c->device));
     HIPCALL(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCALL(hipStreamSynchronize(c->stream));
-    return SDK_OK;
+    return dn_check_error(c);
 }
 
 int sdk_synchronize(sdk_ctx* c) {
@@ -1011,7 +1052,7 @@ int sdk_synchronize(sdk_ctx* c) {
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
     HIPCALL(hipStreamSynchronize(c->stream));
-    return SDK_OK;
+    return dn_check_error(c);
 }
 
 int sdk_timer_reset(sdk_ctx* c) {
@@ -1113,9 +1154,16 @@ int sdk_solve_batch(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell_ma
 
 int sdk_solve_batch_budget(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell_mask, uint8_t* out,
                            int8_t* status, uint64_t* work, size_t n, uint64_t node_budget) {
+    return sdk_solve_batch_ex(c, in, first_cell_mask, out, status, work, n, node_budget, SDK_DONATE_CONTEXT);
+}
+
+int sdk_solve_batch_ex(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell_mask, uint8_t* out, int8_t* status,
+                       uint64_t* work, size_t n, uint64_t node_budget, int64_t donate) {
     if (!c || (n && (!in || !out || !status))) return fail(SDK_EINVAL, "NULL argument");
     if (node_budget != SDK_BUDGET_CONTEXT && node_budget > (uint64_t)INT64_MAX)
         return fail(SDK_EINVAL, "node budget out of range");
+    if (donate < SDK_DONATE_CONTEXT || donate > (1 << 30))
+        return fail(SDK_EINVAL, "donate must be SDK_DONATE_CONTEXT, 0, 1 or a split budget >= 2");
     if (n == 0) return SDK_OK;
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
@@ -1128,13 +1176,13 @@ int sdk_solve_batch_budget(sdk_ctx* c, const uint8_t* in, const uint16_t* first_
     rc = launch_solve(c, static_cast<uint8_t*>(c->in.p), first_cell_mask ? static_cast<uint16_t*>(c->mask.p) : nullptr,
                       static_cast<uint8_t*>(c->out.p), static_cast<int8_t*>(c->status.p),
                       work ? static_cast<uint64_t*>(c->work.p) : nullptr, n, 0, 0, nullptr, nullptr, 0, 1, -1,
-                      node_budget == SDK_BUDGET_CONTEXT ? -1 : (int64_t)node_budget);
+                      node_budget == SDK_BUDGET_CONTEXT ? -1 : (int64_t)node_budget, donate);
     if (rc) return rc;
     HIPCALL(hipMemcpyAsync(out, c->out.p, n * 81, hipMemcpyDeviceToHost, c->stream));
     HIPCALL(hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
     if (work) HIPCALL(hipMemcpyAsync(work, c->work.p, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCALL(hipStreamSynchronize(c->stream));
-    return SDK_OK;
+    return dn_check_error(c);
 }
 
 int sdk_count_solutions(sdk_ctx* c, const uint8_t* board, uint64_t limit, uint64_t* count, int8_t* status) {
@@ -1178,10 +1226,60 @@ int sdk_frontier_refine(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t targ
     if (!c) return fail(SDK_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
-    int rc = refine_frontier(c, first, step, target);
+    int rc = refine_frontier(c, first, step, UINT64_MAX, target);
     if (rc) return rc;
     if (size) *size = c->fr_size;
     if (leaves) *leaves = c->fr_leaves;
+    return SDK_OK;
+}
+
+int sdk_frontier_refine_range(sdk_ctx* c, uint64_t lo, uint64_t hi, uint64_t target, uint64_t* size,
+                              uint64_t* leaves) {
+    if (!c) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    int rc = refine_frontier(c, lo, 1, hi, target);
+    if (rc) return rc;
+    if (size) *size = c->fr_size;
+    if (leaves) *leaves = c->fr_leaves;
+    return SDK_OK;
+}
+
+int sdk_frontier_boards_dev(sdk_ctx* c, void** d_boards, uint64_t* size) {
+    if (!c || !d_boards || !size) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->fr_valid) return fail(SDK_EINVAL, "no frontier: call sdk_frontier_build first");
+    *d_boards = c->fr_a.p;
+    *size = c->fr_size;
+    return SDK_OK;
+}
+
+int sdk_frontier_load_dev(sdk_ctx* c, const void* d_boards, uint64_t n) {
+    if (!c || (n && !d_boards)) return fail(SDK_EINVAL, "NULL argument");
+    if (n > kFrontierCap) return fail(SDK_EINVAL, "at most %llu frontier boards", (unsigned long long)kFrontierCap);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    c->fr_valid = false;
+    const char* src = static_cast<const char*>(d_boards);
+    const char* a0 = static_cast<const char*>(c->fr_a.p);
+    if (n && src == a0) {
+        c->fr_size = n;                     // already in place
+    } else if (n && a0 && src > a0 && src < a0 + c->fr_a.bytes) {
+        // a range of the current frontier (overlapping copy): through fr_b
+        int rc;
+        if ((rc = ensure(c->fr_b, n * 81))) return rc;
+        HIPCALL(hipMemcpyAsync(c->fr_b.p, d_boards, n * 81, hipMemcpyDeviceToDevice, c->stream));
+        std::swap(c->fr_a, c->fr_b);
+        c->fr_size = n;
+    } else {
+        int rc;
+        if ((rc = ensure(c->fr_a, std::max<uint64_t>(n, 1) * 81))) return rc;
+        if (n) HIPCALL(hipMemcpyAsync(c->fr_a.p, d_boards, n * 81, hipMemcpyDeviceToDevice, c->stream));
+        c->fr_size = n;
+    }
+    c->fr_leaves = 0;
+    c->fr_levels = 0;
+    c->fr_valid = true;
     return SDK_OK;
 }
 
@@ -1297,6 +1395,41 @@ int sdk_comm_broadcast_dev(sdk_ctx* c, void* d_buf, size_t bytes, int root) {
     HIPCALL(hipSetDevice(c->device));
     NCCLCALL(ncclBroadcast(d_buf, d_buf, bytes, ncclUint8, root, c->comm, c->stream));
     return SDK_OK;
+}
+
+int sdk_comm_p2p_dev(sdk_ctx* c, int nops, const int* ops, const int* peers, void* const* bufs, const size_t* bytes) {
+    if (!c || nops < 0 || (nops && (!ops || !peers || !bufs || !bytes))) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->comm) return fail(SDK_EINVAL, "no communicator: call sdk_comm_init first");
+    for (int k = 0; k < nops; ++k) {
+        if (ops[k] != SDK_COMM_SEND && ops[k] != SDK_COMM_RECV) return fail(SDK_EINVAL, "bad p2p op %d", ops[k]);
+        if (peers[k] < 0 || peers[k] >= c->comm_world || peers[k] == c->comm_rank)
+            return fail(SDK_EINVAL, "bad p2p peer %d (rank %d of %d)", peers[k], c->comm_rank, c->comm_world);
+        if (bytes[k] && !bufs[k]) return fail(SDK_EINVAL, "NULL p2p buffer");
+    }
+    HIPCALL(hipSetDevice(c->device));
+    NCCLCALL(ncclGroupStart());
+    ncclResult_t r = ncclSuccess;
+    for (int k = 0; k < nops && r == ncclSuccess; ++k) {
+        if (!bytes[k]) continue;   // both sides of a pair agree on the size, so both skip
+        r = ops[k] == SDK_COMM_SEND ? ncclSend(bufs[k], bytes[k], ncclUint8, peers[k], c->comm, c->stream)
+                                    : ncclRecv(bufs[k], bytes[k], ncclUint8, peers[k], c->comm, c->stream);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(SDK_ECOMM, "ncclSend/ncclRecv: %s", ncclGetErrorString(r));
+    if (r2 != ncclSuccess) return fail(SDK_ECOMM, "ncclGroupEnd: %s", ncclGetErrorString(r2));
+    return SDK_OK;
+}
+
+int sdk_comm_send_dev(sdk_ctx* c, const void* d_buf, size_t bytes, int peer) {
+    const int op = SDK_COMM_SEND;
+    void* buf = const_cast<void*>(d_buf);
+    return sdk_comm_p2p_dev(c, 1, &op, &peer, &buf, &bytes);
+}
+
+int sdk_comm_recv_dev(sdk_ctx* c, void* d_buf, size_t bytes, int peer) {
+    const int op = SDK_COMM_RECV;
+    return sdk_comm_p2p_dev(c, 1, &op, &peer, &d_buf, &bytes);
 }
 
 int sdk_comm_allgather_dev(sdk_ctx* c, const void* d_send, void* d_recv, size_t bytes) {

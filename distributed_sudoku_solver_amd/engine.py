@@ -152,6 +152,20 @@ class SudokuEngine:
             engines.append(e)
         return engines
 
+    # options a forked engine takes over (everything a caller sets that shapes a solve)
+    _FORK_OPTIONS = (L.SDK_OPT_ORDER, L.SDK_OPT_NODE_BUDGET, L.SDK_OPT_WAVES_PER_CU, L.SDK_OPT_WORK_COUNTER,
+                     L.SDK_OPT_SOLVER, L.SDK_OPT_WAVES_PER_CU2, L.SDK_OPT_SOLVE_CHUNK, L.SDK_OPT_LOCKED,
+                     L.SDK_OPT_XCD_HEADS, L.SDK_OPT_DONATE, L.SDK_OPT_DONATE_MODE, L.SDK_OPT_DONATE_MAX)
+
+    def fork(self):
+        """A second engine on the same device with its own context and stream (same options):
+        its launches never queue behind this one's, and the GPU runs both at once.  A node
+        gives its new batches and its long searches one each (node.py)."""
+        e = SudokuEngine(self.device)
+        for k in self._FORK_OPTIONS:
+            e.set_option(k, self.get_option(k))
+        return e
+
     # -------------------------------------------------------------- plumbing
     def close(self):
         if getattr(self, "ctx", None) is not None:
@@ -214,18 +228,12 @@ class SudokuEngine:
     def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         """uint8[n,81] (+ optional uint16[n] first-cell masks) -> (out uint8[n,81], status int8[n], work).
 
-        budget: search nodes per board for this call (sdk_solve_batch_budget; 0 = unlimited),
-        None = the context's SDK_OPT_NODE_BUDGET.  A board that runs out is SDK_BUDGET_HIT.
+        budget: search nodes per board for this call (0 = unlimited), None = the context's
+        SDK_OPT_NODE_BUDGET.  A board that runs out is SDK_BUDGET_HIT.
         donate: SDK_OPT_DONATE for this call only (0 = one launch, one slot per board: what a
-        bounded slice of search.LexSearch or a node's batch wants), None = the context's."""
-        if donate is not None:
-            old = self.get_option(L.SDK_OPT_DONATE)
-            if int(donate) != old:
-                self.set_option(L.SDK_OPT_DONATE, int(donate))
-                try:
-                    return self.solve_batch(boards, masks, want_work, budget)
-                finally:
-                    self.set_option(L.SDK_OPT_DONATE, old)
+        bounded slice of search.LexSearch or a node's batch wants), None = the context's.
+        Both are arguments of the one sdk_solve_batch_ex call: the shared context options are
+        never touched, so threads sharing an engine cannot see each other's settings."""
         boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
         n = boards.shape[0]
         if masks is not None:
@@ -233,14 +241,14 @@ class SudokuEngine:
         out = np.empty_like(boards)
         status = np.empty(n, dtype=np.int8)
         work = np.empty(n, dtype=np.uint64) if want_work else None
-        if budget is None:
-            L.check(self.lib.sdk_solve_batch(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status),
-                                             _ptr(work), n), "sdk_solve_batch")
-        else:
-            if not 0 <= int(budget) < (1 << 63):
-                raise ValueError("budget must be 0 (unlimited) or a positive node count")
-            L.check(self.lib.sdk_solve_batch_budget(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status),
-                                                    _ptr(work), n, int(budget)), "sdk_solve_batch_budget")
+        if budget is not None and not 0 <= int(budget) < (1 << 63):
+            raise ValueError("budget must be 0 (unlimited) or a positive node count")
+        if donate is not None and not 0 <= int(donate) <= (1 << 30):
+            raise ValueError("donate must be 0, 1 or a split budget >= 2")
+        L.check(self.lib.sdk_solve_batch_ex(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status), _ptr(work),
+                                            n, L.SDK_BUDGET_CONTEXT if budget is None else int(budget),
+                                            L.SDK_DONATE_CONTEXT if donate is None else int(donate)),
+                "sdk_solve_batch_ex")
         return out, status, work
 
     def expand(self, boards, masks=None, target=64):
@@ -276,6 +284,29 @@ class SudokuEngine:
                                                    ctypes.byref(cnt), ctypes.byref(fr), ctypes.byref(st)),
                 "sdk_count_solutions_slice")
         return cnt.value, fr.value, st.value
+
+    # frontier records (rebalanced counts move them between ranks)
+    def frontier_boards(self):
+        """(device address, size) of the current frontier's uint8[size][81] records."""
+        p = ctypes.c_void_p()
+        size = ctypes.c_uint64()
+        L.check(self.lib.sdk_frontier_boards_dev(self.ctx, ctypes.byref(p), ctypes.byref(size)),
+                "sdk_frontier_boards_dev")
+        return p.value, size.value
+
+    def frontier_load(self, d_boards, n, offset=0):
+        """The n records at device buffer `d_boards` (+ offset boards) become the current
+        count-mode frontier."""
+        ptr = (d_boards.ptr.value if hasattr(d_boards, "ptr") else int(d_boards)) + 81 * int(offset)
+        L.check(self.lib.sdk_frontier_load_dev(self.ctx, ctypes.c_void_p(ptr), int(n)), "sdk_frontier_load_dev")
+
+    def frontier_refine_range(self, lo, hi, target):
+        """Keep frontier boards [lo, hi) and expand them until they number `target`: (size, leaves)."""
+        size = ctypes.c_uint64()
+        leaves = ctypes.c_uint64()
+        L.check(self.lib.sdk_frontier_refine_range(self.ctx, int(lo), int(hi), int(target), ctypes.byref(size),
+                                                   ctypes.byref(leaves)), "sdk_frontier_refine_range")
+        return size.value, leaves.value
 
     # ------------------------------------------- one-board multi-GPU searches
     def frontier_build(self, board, mask=None, mode=L.SDK_FRONTIER_COUNT, target=0):
@@ -338,6 +369,18 @@ class SudokuEngine:
 
     def comm_broadcast(self, d_buf, nbytes, root):
         L.check(self.lib.sdk_comm_broadcast_dev(self.ctx, d_buf.ptr, int(nbytes), int(root)), "sdk_comm_broadcast_dev")
+
+    def comm_p2p(self, ops):
+        """One grouped ncclSend/ncclRecv: ops = [(L.SDK_COMM_SEND | L.SDK_COMM_RECV, peer,
+        device address or DeviceBuffer, nbytes), ...]."""
+        k = len(ops)
+        if k == 0:
+            return
+        kinds = (ctypes.c_int * k)(*[int(o[0]) for o in ops])
+        peers = (ctypes.c_int * k)(*[int(o[1]) for o in ops])
+        bufs = (ctypes.c_void_p * k)(*[(o[2].ptr.value if hasattr(o[2], "ptr") else int(o[2])) for o in ops])
+        sizes = (ctypes.c_size_t * k)(*[int(o[3]) for o in ops])
+        L.check(self.lib.sdk_comm_p2p_dev(self.ctx, k, kinds, peers, bufs, sizes), "sdk_comm_p2p_dev")
 
     def comm_allgather(self, d_send, d_recv, nbytes):
         L.check(self.lib.sdk_comm_allgather_dev(self.ctx, d_send.ptr, d_recv.ptr, int(nbytes)),

@@ -39,11 +39,13 @@ What changes (GPU-first):
     /solve -> 201 {"solution"}; GET /stats (local counters only); GET /network
     -> {"node": "h:p", "predecessor": [h, p] | null, "neighbor": [h, p] | null}.
   * Every launch is bounded (SURVEY §7 hard parts 2 and 7): a batch gives each
-    board `node_budget` search nodes (sdk_solve_batch_budget), so one hard board
-    cannot hold back the others; a board that hits it is continued alone by a
-    search.LexSearch in slices of one bounded launch each, which the worker
-    interleaves with new batches (the node keeps answering POSTs, /stats and
-    the ring).  A budget hit is never reported as NO_SOLUTION: the range stays
+    board `node_budget` search nodes (sdk_solve_batch_ex), so one hard board
+    cannot hold back the others; a board that hits it is continued by a
+    search.LexSearch in bounded slices (~SLICE_TARGET_S each: launch, expansion and
+    copies) on a search thread of its own, with an engine context of its own
+    (engine.fork(): its own HIP stream), so a new batch never waits behind a slice --
+    the GPU runs both launches at once, and the node keeps answering POSTs, /stats
+    and the ring.  A budget hit is never reported as NO_SOLUTION: the range stays
     open.  If the continued search gives up (`search_limit_s`, or its worklist
     outgrows search.DEFAULT_MAX_PENDING) the range is reported as EXHAUSTED {uuid,
     range, sudoku} (a new method; reference nodes ignore it) and the HTTP origin
@@ -66,14 +68,13 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 import numpy as np
 
 from .engine import ALL_DIGITS_MASK, encode_solve_grid, range_to_mask
-from .search import DEFAULT_MAX_PENDING, DEFAULT_WIDTH, LexSearch, default_budget
+from .search import DEFAULT_MAX_PENDING, DEFAULT_WIDTH, SLICE_TARGET_S, LexSearch, default_budget
 from .utils import split_array_in_middle
 from . import _lib as L
 
 RECV_BYTES = 1024          # DHT_Node.py:82,94
 HEARTBEAT_S = 5.0          # DHT_Node.py:43
 STATS_WAIT_S = 1.0         # DHT_Node.py:571
-SLICE_TARGET_S = 0.01     # wall time of one search slice's launch (search.LexSearch slice_target_s)
 SEARCH_LIMIT_S = 10.0      # a budget-hit task's continued search gives up after this (EXHAUSTED)
 DONE_UUIDS_KEPT = 1 << 16  # answered puzzles remembered (late duplicates are dropped)
 
@@ -131,12 +132,16 @@ def _addr(a):
 
 
 class SudokuNode:
-    """One ring member.  `engine` is a SudokuEngine (or anything with solve_batch)."""
+    """One ring member.  `engine` is a SudokuEngine, a shard.MultiDeviceEngine (every GPU of
+    the box: each drained batch and each search slice is sharded over them), or anything with
+    solve_batch / expand.  `search_engine` continues budget-hit boards (default: engine.fork(),
+    a second context on the same devices, or the engine itself if it cannot fork)."""
 
     def __init__(self, host, p2p_port, http_port, anchor=None, engine=None, delay_ms=0.0,
                  heartbeat_s=HEARTBEAT_S, stats_wait_s=STATS_WAIT_S, solve_timeout_s=600.0, log=False,
                  api="dht", split=True, trace=False, node_budget=None, search_limit_s=SEARCH_LIMIT_S,
-                 search_width=DEFAULT_WIDTH, search_max_pending=DEFAULT_MAX_PENDING):
+                 search_width=DEFAULT_WIDTH, search_max_pending=DEFAULT_MAX_PENDING, search_engine=None,
+                 slice_target_s=SLICE_TARGET_S):
         if api not in ("dht", "main"):
             raise ValueError("api must be 'dht' (DHT_Node.py) or 'main' (main.py)")
         self.api = api
@@ -156,11 +161,18 @@ class SudokuNode:
         self.search_limit_s = float(search_limit_s)
         self.search_width = int(search_width)
         self.search_max_pending = int(search_max_pending)
+        self.slice_target_s = float(slice_target_s)
         self.log = log
         if engine is None:
             from .solver import default_engine
             engine = default_engine()
         self.engine = engine
+        if search_engine is None:
+            search_engine = engine.fork() if hasattr(engine, "fork") else engine
+            self._own_search_engine = search_engine is not engine      # made here: closed by stop()
+        else:
+            self._own_search_engine = False
+        self.search_engine = search_engine
         self.node_budget = self._node_budget or default_budget(engine)   # per board per launch
         # ring state (guarded by self.lock)
         self.lock = threading.RLock()
@@ -174,8 +186,9 @@ class SudokuNode:
         # work state
         self.tasks = queue.Queue()               # pending TASK dicts
         self.neighbor_tasks = []                 # tasks handed to the neighbour (re-run on its failure)
-        self.hard = []                           # _HardTask: budget-hit tasks continued between batches
-        self.busy = False
+        self.hard = []                           # _HardTask: budget-hit tasks (the search thread's round robin)
+        self.busy = False                        # the worker runs a batch
+        self.searching = False                   # the search thread runs a slice
         self.done_uuids = _RecentSet()           # uuids already solved somewhere in the ring
         self.best = {}                           # uuid -> (lowest digit, grid): best ordered completion (origin only)
         self.waiters = {}                        # uuid -> (Event, [solution], puzzle, [failed mask, exhausted mask])
@@ -221,7 +234,8 @@ class SudokuNode:
                 self.network = [self.me]
                 self.coordinator = self.predecessor = self.neighbor = self.me
                 self.inside = True
-        for target in (self._udp_loop, self._worker_loop, self._heartbeat_loop, self.httpd.serve_forever):
+        for target in (self._udp_loop, self._worker_loop, self._search_loop, self._heartbeat_loop,
+                       self.httpd.serve_forever):
             t = threading.Thread(target=target, daemon=True)
             t.start()
             self._threads.append(t)
@@ -251,6 +265,13 @@ class SudokuNode:
         self.httpd.shutdown()
         self.httpd.server_close()
         self.sock.close()
+        if self._own_search_engine:
+            # the search thread ends after its current (bounded) slice; then its context goes
+            for t in self._threads:
+                if t is not threading.current_thread():
+                    t.join(timeout=5.0)
+            if not any(t.is_alive() for t in self._threads if t is not threading.current_thread()):
+                self.search_engine.close()
 
     # ------------------------------------------------------------- UDP side
     def _udp_loop(self):
@@ -340,14 +361,14 @@ class SudokuNode:
             self.inside = True
             self.neighborfree = False
             self.last_heartbeat = time.time()
-            idle = not self.busy and self.tasks.empty()
+            idle = self._idle_locked()
         if idle and self.predecessor != self.me:
             self.send({"method": "NEEDWORK"}, self.predecessor)
 
     def _on_UPDATE_PREDECESSOR(self, msg):
         with self.lock:
             self.predecessor = _addr(msg["predecessor"])
-            idle = not self.busy and self.tasks.empty()
+            idle = self._idle_locked()
         if idle and self.predecessor != self.me:
             self.send({"method": "NEEDWORK"}, self.predecessor)
 
@@ -437,7 +458,7 @@ class SudokuNode:
         if busy:                 # an idle neighbour takes what would wait behind the running batch
             self._maybe_delegate()
         with self._work:
-            self._work.notify()
+            self._work.notify_all()
 
     def _drain_queue(self):
         out = []
@@ -479,39 +500,65 @@ class SudokuNode:
     def resume(self):
         self._go.set()
         with self._work:
-            self._work.notify()
+            self._work.notify_all()
+
+    def _idle_locked(self):
+        return self.tasks.empty() and not self.hard and not self.busy and not self.searching
 
     def _worker_loop(self):
-        """New TASKs first (one batched launch per drained queue); between batches, one slice of
-        the oldest budget-hit search (round robin), so a long search never delays new puzzles by
-        more than one bounded launch."""
+        """New TASKs: one batched launch per drained queue.  Budget-hit boards go to the search
+        thread, so a batch never waits for a long search."""
         while self.running:
             with self._work:
-                while self.running and ((self.tasks.empty() and not self.hard) or not self._go.is_set()):
+                while self.running and (self.tasks.empty() or not self._go.is_set()):
                     self._work.wait(0.5)
             if not self.running:
                 return
             with self.lock:
                 batch = [t for t in self._drain_queue() if t.get("uuid") not in self.done_uuids]
-                hard = None if batch or not self.hard else self.hard.pop(0)
-                self.busy = True
-            work = batch if batch else ([hard.task] if hard else [])
+                self.busy = bool(batch)
+            if not batch:
+                continue
             try:
-                if batch:
-                    self._run_batch(batch)
-                elif hard:
-                    self._run_slice(hard)
+                self._run_batch(batch)
             except Exception as e:      # the worker must survive a failed launch (ADVICE r1)
                 self._log("launch failed:", repr(e))
-                for t in work:
+                for t in batch:
                     self._wake(t.get("uuid"), "error", error=repr(e))
             finally:
                 with self.lock:
                     self.busy = False
                     pred = self.predecessor
-                    idle = self.tasks.empty() and not self.hard
+                    idle = self._idle_locked()
             if idle and pred and pred != self.me:
                 self.send({"method": "NEEDWORK"}, pred)        # DHT_Node.py:245-248
+
+    def _search_loop(self):
+        """Budget-hit searches, one bounded slice at a time, round robin (search.LexSearch on the
+        node's search engine: its own context and stream, beside the worker's batches)."""
+        while self.running:
+            with self._work:
+                while self.running and not self.hard:
+                    self._work.wait(0.5)
+            if not self.running:
+                return
+            with self.lock:
+                h = self.hard.pop(0) if self.hard else None
+                self.searching = h is not None
+            if h is None:
+                continue
+            try:
+                self._run_slice(h)
+            except Exception as e:      # a failed slice answers its POST with 500; the thread goes on
+                self._log("search slice failed:", repr(e))
+                self._wake(h.task.get("uuid"), "error", error=repr(e))
+            finally:
+                with self.lock:
+                    self.searching = False
+                    pred = self.predecessor
+                    idle = self._idle_locked()
+            if idle and pred and pred != self.me:
+                self.send({"method": "NEEDWORK"}, pred)
 
     def _split_for_neighbor(self, batch):
         """DHT_Node.py:491-510 at launch time: a free neighbour gets the upper half of the
@@ -553,11 +600,14 @@ class SudokuNode:
         self._spent(int(np.asarray(work).sum()))
         for t, b, m, o, st in zip(batch, boards, masks, out, status):
             if st == L.SDK_BUDGET_HIT:
-                # not "no solution": the subtree is unexplored.  Continue it alone, between batches
-                s = LexSearch(self.engine, b, int(m), budget=self.node_budget, width=self.search_width,
-                              max_pending=self.search_max_pending, hit=True, slice_target_s=SLICE_TARGET_S)
+                # not "no solution": the subtree is unexplored.  Continue it on the search thread
+                s = LexSearch.for_node(self.search_engine, b, int(m), budget=self.node_budget,
+                                       width=self.search_width, max_pending=self.search_max_pending,
+                                       slice_target_s=self.slice_target_s)
                 with self.lock:
                     self.hard.append(_HardTask(t, s, time.monotonic() + self.search_limit_s))
+                with self._work:
+                    self._work.notify_all()
                 self._log("budget hit, continuing", t.get("uuid"))
             else:
                 self._task_done(t, int(st), o)
@@ -577,7 +627,8 @@ class SudokuNode:
             self._task_done(h.task, int(h.search.status), h.search.board)
         else:
             with self.lock:
-                self.hard.append(h)
+                if h.task.get("uuid") not in self.done_uuids:
+                    self.hard.append(h)
 
     def _task_done(self, t, st, o):
         """Report a finished task: its completion, 'no completion in this range' (NO_SOLUTION) or

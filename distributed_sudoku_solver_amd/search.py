@@ -26,10 +26,19 @@ product-path solve here is bounded:
     deadline passes, ends as SDK_BUDGET_HIT ("search exhausted"): a defined answer that
     is never confused with "no completion" (node.py keeps digit ranges lex-ordered on it).
 
-A slice is one launch plus at most one expansion call, so a node's worker can
-interleave new requests with a long search between slices (node.py).  The search
-runs on whatever engine it is given: SudokuEngine (libsudoku_hip.so) in the product,
-an oracle double in the CPU tests.
+A slice is one launch plus at most one expansion call.  With a slice target (a node's
+continued search, LexSearch.for_node) every part of a slice is bounded before it runs, and
+the whole slice -- launch, expansion, host copies -- is what is measured against it:
+  * the first slice runs at the smallest budget;
+  * the launch's node budget is capped by the measured wall time per search node on a
+    launch's critical path (launch time / most nodes any board took), so budget x that
+    time stays within LAUNCH_SHARE of the target; at budget 1 the width shrinks instead;
+  * the number of budget hits expanded per slice halves while an expansion takes more than
+    EXPAND_SHARE_OF_TARGET of the target.
+A node runs these slices on their own thread and engine context (node.py), so new requests
+never wait behind one.  The search runs on whatever engine it is given: SudokuEngine
+(libsudoku_hip.so) in the product, a MultiDeviceEngine (the slice's launch and expansion
+sharded over every GPU of the node), an oracle double in the CPU tests.
 """
 import collections
 import time
@@ -45,6 +54,15 @@ DEFAULT_MAX_PENDING = 1 << 20  # sub-boards the worklist may hold (81 MB of host
 BUDGET_GROWTH_CAP = 8          # the per-launch budget may double up to this multiple of the first
 EXPAND_SHARE = 32              # a slice expands at most width / this of its hits (the lex front)
 LANE_VALIDATIONS_PER_NODE = 4096   # SDK_SOLVER_LANE budgets count the reference's validations
+SLICE_TARGET_S = 0.01          # a node's continued search: wall time of one slice (search + expansion + copies)
+LAUNCH_SHARE = 0.5             # ... of which the launch may take this much (budget x node time)
+EXPAND_SHARE_OF_TARGET = 0.3   # ... and an expansion this much before fewer hits are expanded
+MIN_WIDTH = 256                # sub-boards per slice, at least (per device)
+
+
+def n_devices(engine):
+    """GPUs an engine drives (MultiDeviceEngine: all of them; anything else: one)."""
+    return max(1, int(getattr(engine, "n_devices", 1)))
 
 
 def default_budget(engine):
@@ -85,6 +103,10 @@ class LexSearch:
         # much longer than this between two batches of new puzzles.
         self.slice_target_s = None if slice_target_s is None else float(slice_target_s)
         self.min_budget = max(1, self.budget // BUDGET_GROWTH_CAP)
+        self.t_node = None        # wall time per search node on a launch's critical path (measured)
+        self.expand_cap = max(1, self.width // EXPAND_SHARE)   # budget hits expanded per slice, at most
+        self.last_slice_s = 0.0   # wall time of the last slice, all of it
+        self.max_slice_s = 0.0
         self.max_pending = int(max_pending)
         root_mask = ALL_DIGITS_MASK if mask is None else int(mask)
         # worklist: chunks (boards uint8[k,81], masks uint16[k]) in lex order of their subtrees
@@ -97,6 +119,19 @@ class LexSearch:
         self.launches = 0
         self.expansions = 0
         self.slices = 0
+
+    @classmethod
+    def for_node(cls, engine, board, mask=None, budget=None, width=None, max_pending=DEFAULT_MAX_PENDING,
+                 slice_target_s=SLICE_TARGET_S):
+        """A board whose batch launch hit the node budget, continued in slices of about
+        slice_target_s each (node.py): DEFAULT_WIDTH sub-boards per device and slice, the first
+        slice at the smallest budget, the later ones at what the measured node time allows."""
+        b = default_budget(engine) if budget is None else int(budget)
+        w = (DEFAULT_WIDTH if width is None else int(width)) * n_devices(engine)
+        s = cls(engine, board, mask, budget=b, width=w, max_pending=max_pending, hit=True,
+                slice_target_s=slice_target_s)
+        s.budget = s.min_budget
+        return s
 
     # ----------------------------------------------------------------- worklist
     def _take(self, k):
@@ -121,8 +156,16 @@ class LexSearch:
             self._pending += len(boards)
 
     def _expand(self, boards, masks):
+        t0 = time.monotonic()
         kids = self.engine.expand(boards, masks, target=max(self.width, 2 * len(boards)))
         self.expansions += 1
+        if self.slice_target_s is not None:
+            # fewer hits per expansion while one takes a large share of the slice
+            dt = time.monotonic() - t0
+            if dt > EXPAND_SHARE_OF_TARGET * self.slice_target_s:
+                self.expand_cap = max(1, self.expand_cap // 2)
+            elif 3 * dt < EXPAND_SHARE_OF_TARGET * self.slice_target_s:
+                self.expand_cap = min(max(1, self.width // EXPAND_SHARE), 2 * self.expand_cap)
         return kids, np.full(len(kids), ALL_DIGITS_MASK, np.uint16)   # a mask lives in level 0 only
 
     @property
@@ -147,6 +190,14 @@ class LexSearch:
         """One slice: one launch over the worklist's front (+ one expansion call).  Returns done."""
         if self.status is not None:
             return True
+        t_slice = time.monotonic()
+        try:
+            return self._step()
+        finally:
+            self.last_slice_s = time.monotonic() - t_slice
+            self.max_slice_s = max(self.max_slice_s, self.last_slice_s)
+
+    def _step(self):
         self.slices += 1
         if self._expand_first:
             self._expand_first = False
@@ -162,7 +213,13 @@ class LexSearch:
         elapsed = time.monotonic() - t0
         self.launches += 1
         if work is not None:
-            self.nodes += int(np.asarray(work, dtype=np.uint64).sum())
+            work = np.asarray(work, dtype=np.uint64)
+            self.nodes += int(work.sum())
+            if self.slice_target_s is not None and len(work):
+                # launch wall time per node of its longest board (its critical path): an upper
+                # bound of the node time, so the budget derived from it keeps the launch short
+                tn = elapsed / max(1, int(work.max()))
+                self.t_node = tn if self.t_node is None else max(tn, 0.5 * (self.t_node + tn))
         st = np.asarray(st)
         decided = np.flatnonzero(st != L.SDK_UNSOLVABLE)          # refuted sub-boards simply vanish
         solved = decided[st[decided] == L.SDK_SOLVED]
@@ -174,15 +231,14 @@ class LexSearch:
             self._chunks.clear()
             self._pending = 0
         if len(hits):
-            k = min(len(hits), max(1, self.width // EXPAND_SHARE))
+            k = min(len(hits), self.expand_cap if self.slice_target_s is not None else max(1, self.width // EXPAND_SHARE))
             self._push_front(boards[hits[k:]], masks[hits[k:]])           # retried later, unexpanded
             self._push_front(*self._expand(boards[hits[:k]], masks[hits[:k]]))
-            slow = self.slice_target_s is not None and elapsed > self.slice_target_s
-            fast = self.slice_target_s is None or 2 * elapsed < self.slice_target_s
-            if slow:
-                self.budget = max(self.min_budget, self.budget // 2)
-            elif fast and 2 * len(hits) > len(boards):
-                self.budget = min(2 * self.budget, self.max_budget)
+            if self.slice_target_s is None:
+                if 2 * len(hits) > len(boards):
+                    self.budget = min(2 * self.budget, self.max_budget)
+            else:
+                self._bound_budget(elapsed, 2 * len(hits) > len(boards))
         if self._pending == 0:
             self._finish(L.SDK_SOLVED if self.best is not None else L.SDK_UNSOLVABLE)
             return True
@@ -190,6 +246,21 @@ class LexSearch:
             self._finish(L.SDK_BUDGET_HIT)
             return True
         return False
+
+    def _bound_budget(self, launch_s, mostly_hits):
+        """The next launch's budget (and width) under the slice target: grow while launches are
+        fast and mostly hit the budget, halve after a slow one, and never above what the
+        measured node time allows for LAUNCH_SHARE of the target."""
+        target = self.slice_target_s
+        if launch_s > LAUNCH_SHARE * target:
+            self.budget = max(1, self.budget // 2)
+        elif 2 * launch_s < LAUNCH_SHARE * target and mostly_hits:
+            self.budget = min(2 * self.budget, self.max_budget)
+        if self.t_node:
+            self.budget = max(1, min(self.budget, int(LAUNCH_SHARE * target / self.t_node)))
+        if self.budget == 1 and launch_s > LAUNCH_SHARE * target:
+            # one node per board is still too long: the launch's fixed costs (copies) dominate
+            self.width = max(MIN_WIDTH * n_devices(self.engine), self.width // 2)
 
     def run(self, deadline=None):
         """Slices until done or time.monotonic() passes `deadline` (then SDK_BUDGET_HIT)."""

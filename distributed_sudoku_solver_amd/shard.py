@@ -109,7 +109,10 @@ class ShardedBatch:
 
 def _run_per_device(items, body):
     """body(k, item) on one host thread per item (ctypes drops the GIL inside every
-    library call, so the devices run concurrently); first exception re-raised."""
+    library call, so the devices run concurrently); first exception re-raised.  A single
+    item runs on the calling thread."""
+    if len(items) == 1:
+        return [body(0, items[0])]
     errors = []
     results = [None] * len(items)
 
@@ -134,11 +137,37 @@ class MultiDeviceEngine:
     one host thread per device.  Batches go to disjoint output slices (no
     collectives); with `open_clique` the engines also share one RCCL communicator
     (ncclCommInitAll, sdk_comm_init_all) for the one-board frontier searches --
-    the torch-free single-process form of SURVEY §8(e)."""
+    the torch-free single-process form of SURVEY §8(e).
+
+    It has the engine surface a node drives (solve_batch with per-call budget and donate,
+    expand, fork, get_option), so node.SudokuNode runs on every GPU of the box -- the
+    in-node replacement of DHT_Node's network work-splitting (DHT_Node.py:491-510, 225-250):
+    each drained TASK batch is sharded over the devices, and a budget-hit board's continued
+    search (search.LexSearch) shards every slice's launch and expansion over them."""
 
     def __init__(self, engines, comms=None):
         self.engines = list(engines)
+        if not self.engines:
+            raise ValueError("MultiDeviceEngine needs at least one engine")
         self.comms = comms
+
+    @property
+    def n_devices(self):
+        return len(self.engines)
+
+    def get_option(self, key):
+        return self.engines[0].get_option(key)
+
+    def set_option(self, key, value):
+        for e in self.engines:
+            e.set_option(key, value)
+
+    def fork(self):
+        """Second contexts on the same devices (no communicator): a node's search engine.
+        Engines that cannot fork (test doubles) are shared: then this engine itself."""
+        if not all(hasattr(e, "fork") for e in self.engines):
+            return self
+        return MultiDeviceEngine([e.fork() for e in self.engines])
 
     @classmethod
     def open(cls, devices):
@@ -154,16 +183,20 @@ class MultiDeviceEngine:
 
     def close(self):
         for e in self.engines:
-            e.close()
+            if hasattr(e, "close"):
+                e.close()
+
+    def _parts(self, n):
+        """(engine, lo, hi) of every device with a non-empty contiguous share of n units."""
+        G = len(self.engines)
+        parts = [(e,) + shard_bounds(n, k, G) for k, e in enumerate(self.engines)]
+        return [p for p in parts if p[2] > p[1]]
 
     def _run(self, n, work):
-        def body(k, eng):
-            lo, hi = shard_bounds(n, k, len(self.engines))
-            if hi > lo:
-                work(eng, lo, hi)
-        _run_per_device(self.engines, body)
+        _run_per_device(self._parts(n), lambda k, p: work(*p))
 
-    def solve_batch(self, boards, masks=None, want_work=False):
+    def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
+        """Contiguous shards, one per device, one launch each (same budget / donate)."""
         boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
         n = boards.shape[0]
         out = np.empty_like(boards)
@@ -172,13 +205,31 @@ class MultiDeviceEngine:
 
         def work(eng, lo, hi):
             m = None if masks is None else np.asarray(masks, dtype=np.uint16)[lo:hi]
-            o, s, w = eng.solve_batch(boards[lo:hi], m, want_work)
+            o, s, w = eng.solve_batch(boards[lo:hi], m, want_work, budget=budget, donate=donate)
             out[lo:hi], st[lo:hi] = o, s
             if want_work:
                 wk[lo:hi] = w
 
         self._run(n, work)
         return out, st, wk
+
+    def expand(self, boards, masks=None, target=64):
+        """Ordered frontier below `boards`, the parents split contiguously over the devices:
+        device k expands its parents towards its share of `target`, and the children are
+        concatenated in device order -- parents' order kept, so still the ordered partition of
+        the parents' completions that search.LexSearch needs."""
+        boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
+        n = boards.shape[0]
+        parts = self._parts(n)
+        kids = [None] * len(parts)
+
+        def body(k, p):
+            eng, lo, hi = p
+            m = None if masks is None else np.asarray(masks, dtype=np.uint16)[lo:hi]
+            kids[k] = eng.expand(boards[lo:hi], m, target=max(1, -(-int(target) * (hi - lo) // n)))
+
+        _run_per_device(parts, body)
+        return np.concatenate(kids) if kids else np.zeros((0, 81), np.uint8)
 
     def check_batch(self, boards):
         boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)

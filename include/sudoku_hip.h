@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define SDK_ABI_VERSION 1
+#define SDK_ABI_VERSION 2   /* 2: sdk_solve_batch_ex, frontier records, p2p send/recv */
 
 /* return codes */
 #define SDK_OK        0
@@ -104,6 +104,11 @@ extern "C" {
                                  /* (default 2^19; 0 = any size): a larger batch is one  */
                                  /* launch, where its heavy boards are a small share of  */
                                  /* the time (1M minimal puzzles: the phases cost 6 %)   */
+#define SDK_OPT_DN_FAULT     21  /* test only: 1 = idle waves of the donation kernel skip */
+                                 /* writing their registration entry, so a donor's       */
+                                 /* bounded wait for it runs out: the solve then fails   */
+                                 /* with SDK_EHIP (every wait on another wave inside a   */
+                                 /* launch is bounded and reports this way)              */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */
@@ -173,6 +178,16 @@ int sdk_solve_batch(sdk_ctx *ctx, const uint8_t *in, const uint16_t *first_cell_
 int sdk_solve_batch_budget(sdk_ctx *ctx, const uint8_t *in, const uint16_t *first_cell_mask,
                            uint8_t *out, int8_t *status, uint64_t *work, size_t n, uint64_t node_budget);
 
+/* sdk_solve_batch_budget with this call's SDK_OPT_DONATE as well (SDK_DONATE_CONTEXT = the
+ * context's; 0 = one launch, one slot per board; 1 or a split budget >= 2 = the phased
+ * solve with subtree donation).  Threads sharing a context (ring nodes on one GPU, a node's
+ * batch and search threads) pick the launch shape per call without touching the shared
+ * option. */
+#define SDK_DONATE_CONTEXT -1
+int sdk_solve_batch_ex(sdk_ctx *ctx, const uint8_t *in, const uint16_t *first_cell_mask,
+                       uint8_t *out, int8_t *status, uint64_t *work, size_t n, uint64_t node_budget,
+                       int64_t donate);
+
 /* The worklist step of a resumable lex-first search of a board whose solve hit the
  * budget (distributed_sudoku_solver_amd/search.py; the in-node form of handing a
  * subtree on, DHT_Node.py:491-510): expand n boards -- board i with first-cell mask
@@ -240,6 +255,23 @@ int sdk_frontier_count_dev(sdk_ctx *ctx, uint64_t first, uint64_t step, uint64_t
  * (device, 82 bytes: board[81], int8 status). */
 int sdk_frontier_first_dev(sdk_ctx *ctx, uint64_t lo, uint64_t hi, void *d_found, void *d_best);
 
+/* Frontier records, for moving live subtrees between ranks (SURVEY §8(e) rebalance; the
+ * device form of the reference handing a partial board on mid-search, DHT_Node.py:502-509):
+ *   sdk_frontier_boards_dev   *d_boards = device address of the current frontier's
+ *                             uint8[*size][81] records (valid until the next frontier call
+ *                             on this context); send a range of it with sdk_comm_send_dev.
+ *   sdk_frontier_load_dev     the n records at d_boards (device, e.g. received with
+ *                             sdk_comm_recv_dev) become the current count-mode frontier
+ *                             (copied; 0 leaves).
+ *   sdk_frontier_refine_range keep frontier boards [lo, hi) and expand them on this device
+ *                             until they number `target` (or nothing branches): a rank splits
+ *                             its last heavy subtree into second-level records.  *leaves =
+ *                             completions met while refining. */
+int sdk_frontier_boards_dev(sdk_ctx *ctx, void **d_boards, uint64_t *size);
+int sdk_frontier_load_dev(sdk_ctx *ctx, const void *d_boards, uint64_t n);
+int sdk_frontier_refine_range(sdk_ctx *ctx, uint64_t lo, uint64_t hi, uint64_t target, uint64_t *size,
+                              uint64_t *leaves);
+
 /* RCCL communicator bound to a context (one rank per GPU).  Rank 0 makes the
  * id, the caller distributes it (e.g. over torch.distributed/gloo), every rank
  * calls sdk_comm_init (collective, blocks until all ranks joined). */
@@ -265,6 +297,17 @@ int sdk_comm_broadcast_dev(sdk_ctx *ctx, void *d_buf, size_t bytes, int root);
 /* d_recv[r*bytes .. (r+1)*bytes) = rank r's d_send (ncclAllGather): the live-range
  * exchange of the rebalanced frontier count (shard.sharded_count_rebalanced). */
 int sdk_comm_allgather_dev(sdk_ctx *ctx, const void *d_send, void *d_recv, size_t bytes);
+/* Point-to-point on device memory (ncclSend / ncclRecv inside one ncclGroupStart/End):
+ * the frontier-record moves of the rebalanced count.  sdk_comm_p2p_dev issues `nops`
+ * operations as one group: ops[k] = SDK_COMM_SEND (bufs[k] -> rank peers[k]) or
+ * SDK_COMM_RECV (rank peers[k] -> bufs[k]), bytes[k] each (a matching pair of calls on
+ * the two ranks must agree on the size). */
+#define SDK_COMM_SEND 0
+#define SDK_COMM_RECV 1
+int sdk_comm_send_dev(sdk_ctx *ctx, const void *d_buf, size_t bytes, int peer);
+int sdk_comm_recv_dev(sdk_ctx *ctx, void *d_buf, size_t bytes, int peer);
+int sdk_comm_p2p_dev(sdk_ctx *ctx, int nops, const int *ops, const int *peers, void *const *bufs,
+                     const size_t *bytes);
 
 /* ---- device-pointer API (asynchronous on the context stream) ------------ */
 int sdk_dev_alloc(sdk_ctx *ctx, size_t bytes, void **dptr);

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(L.LIB_PATH)
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert L.load().sdk_abi_version() == 1
+    assert L.load().sdk_abi_version() == L.SDK_ABI_VERSION == 2
 
 
 def test_library_is_gfx950_code_object():

@@ -213,3 +213,73 @@ def test_large_batch_with_hard_tail(engine, mode):
     out, st, _, _ = _solve(engine, boards, mode=mode)
     assert (st == 1).all()
     assert (out[:len(p17)] == s17).all() and (out[len(p17):] == sh).all()
+
+
+def test_bounded_wait_reports_an_error(engine):
+    """Every wait on another wave inside a donation launch is bounded (solve4_kernel.h
+    kDnWaitTicks).  SDK_OPT_DN_FAULT (test only) makes idle waves skip writing their
+    registration entry, so a donor's wait for it runs out: the launch still ends, the solve
+    fails with SDK_EHIP naming the wait, and the next solve on the context is exact again."""
+    fork = engine.fork()
+    try:
+        p, s, _ = _heavy_minimal(fork, 20000, 64, seed=3)
+        fork.set_option(L.SDK_OPT_DN_FAULT, 1)
+        assert fork.get_option(L.SDK_OPT_DN_FAULT) == 1
+        with pytest.raises(L.SudokuHipError, match="bounded wait"):
+            _solve(fork, p)
+        fork.set_option(L.SDK_OPT_DN_FAULT, 0)
+        out, st, _, donated = _solve(fork, p)
+        assert donated > 0 and (st == 1).all() and (out == s).all()
+    finally:
+        fork.close()
+
+
+def test_donation_beside_another_context_on_the_gpu(engine):
+    """a donation launch must end whether or not its whole grid is resident at
+    once.  Two contexts on one GPU run phased solves of the heavy boards at the same time (each
+    launch's grid is the full resident grid, so neither fits beside the other); both finish
+    promptly and exactly.  Round 3's kernel, which waited for the whole grid to be counted idle,
+    took seconds here (profiles/r03/bench_2rank_shared_gpu.json: 4,155 ms for a 2 ms solve)."""
+    import threading
+    import time
+    p, s, _ = _heavy_minimal(engine, 20000, 1000, seed=21)
+    engines = [engine.fork(), engine.fork()]
+    res, errs = {}, []
+
+    def run(k):
+        try:
+            t0 = time.perf_counter()
+            for _ in range(5):
+                out, st, _, _ = _solve(engines[k], p)
+                assert (st == 1).all() and (out == s).all()
+            res[k] = time.perf_counter() - t0
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            errs.append(e)
+
+    try:
+        ths = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(120)
+        assert not errs, errs
+        assert len(res) == 2 and max(res.values()) < 3.0, res
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_per_call_donate_leaves_the_context_option(engine):
+    """solve_batch(donate=...) is one sdk_solve_batch_ex argument; the context's
+    SDK_OPT_DONATE is never rewritten (threads sharing an engine cannot see each other's)."""
+    p, s, _ = _heavy_minimal(engine, 20000, 64, seed=3)
+    engine.set_option(L.SDK_OPT_DONATE_MAX, 0)
+    try:
+        assert engine.get_option(L.SDK_OPT_DONATE) == 1
+        out, st, _ = engine.solve_batch(p, donate=SPLIT)
+        assert engine.get_option(L.SDK_OPT_DONATE) == 1 and engine.get_option(L.SDK_OPT_SPLIT_BOARDS) == len(p)
+        assert (st == 1).all() and (out == s).all()
+        out, st, _ = engine.solve_batch(p, donate=0)
+        assert engine.get_option(L.SDK_OPT_SPLIT_BOARDS) == 0 and (out == s).all()
+    finally:
+        engine.set_option(L.SDK_OPT_DONATE_MAX, 1 << 19)

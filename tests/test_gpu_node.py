@@ -202,3 +202,31 @@ def test_graceful_stop_hands_queue_back_on_gpu(engine):
     from test_node import OracleEngine, graceful_stop_scenario
     graceful_stop_scenario(OracleEngine(), engine)
     graceful_stop_scenario(engine, engine)
+
+
+# ------------------------------------------------------- every GPU of the box (north_star; N3)
+def test_node_on_the_clique(engine):
+    """A SudokuNode on MultiDeviceEngine.open_clique (every GPU of the box; one here): batches and
+    the continued search of budget-hit boards are sharded over the clique's devices, on a second
+    set of contexts for the search.  Wiki, DEMO8's golden lex-first board through a budget-hit
+    continued search, and the documented 504 for '55'+79 zeros."""
+    import threading
+    from distributed_sudoku_solver_amd.shard import MultiDeviceEngine
+    from test_node import CONFLICT55, DEMO8, DEMO8_FIRST, _post_any
+    mde = MultiDeviceEngine.open_clique([0])
+    node = SudokuNode("127.0.0.1", 0, 0, engine=mde, delay_ms=0, node_budget=1, search_limit_s=3.0).start()
+    try:
+        assert node.search_engine is not mde and node.search_engine.n_devices == mde.n_devices
+        code, body = _post(node.http_port, _grid(synth.WIKI))
+        assert code == 201 and "".join(str(v) for row in body["solution"] for v in row) == synth.WIKI_SOLUTION
+        code, body = _post(node.http_port, _grid(DEMO8))
+        assert code == 201 and "".join(str(v) for row in body["solution"] for v in row) == DEMO8_FIRST
+        res = {}
+        th = threading.Thread(target=lambda: res.__setitem__("c", _post_any(node.http_port, _grid(CONFLICT55))))
+        th.start()
+        th.join(60)
+        code, body = res["c"]
+        assert code == 504 and body["exhausted"] is True and body["solution"] is None
+    finally:
+        _stop([node])
+        mde.close()

@@ -121,7 +121,7 @@ def test_conflict55_exhausts_quickly(engine):
     st, out = s.run(time.monotonic())                   # deadline passed: exhausted
     assert st == L.SDK_BUDGET_HIT and (out == b).all()
     assert time.perf_counter() - t0 < 4.0
-    assert len(slices) > 3 and max(slices) < 0.25, (len(slices), max(slices), s.budget, s.pending)
+    assert len(slices) > 3 and max(slices) < 0.25, (len(slices), max(slices), s.budget, s.pending)   # unbounded mode
     batch = np.stack([b, synth.parse(synth.WIKI)])
     t0 = time.perf_counter()
     out, st, _ = engine.solve_batch(batch, want_work=True, budget=2048)
@@ -140,3 +140,24 @@ def test_dropin_solve_grid_is_bounded(engine):
     grid = [list(map(int, synth.SEEDS17["S2"][9 * r: 9 * r + 9])) for r in range(9)]
     ok, _ = solve_grid(grid, engine=engine, budget=1)
     assert ok and "".join(str(v) for row in grid for v in row) == synth.SEED_SOLUTIONS["S2"]
+
+
+def test_node_slices_are_bounded(engine):
+    """a node's continued search (LexSearch.for_node, on its own context) keeps
+    every slice -- launch, expansion and host copies together -- within 1.5 x the slice target,
+    on '55'+79 zeros (unrefutable: every sub-board hits the budget, the worst case)."""
+    from distributed_sudoku_solver_amd.search import SLICE_TARGET_S
+    fork = engine.fork()
+    try:
+        b = synth.parse(CONFLICT55)
+        s = LexSearch.for_node(fork, b)
+        s.step()                                        # warm: the first slice sizes the buffers
+        times = []
+        for _ in range(30):
+            s.step()
+            times.append(s.last_slice_s)
+        assert not s.done
+        assert max(times) <= 1.5 * SLICE_TARGET_S, (["%.2f" % (1e3 * t) for t in times], s.budget, s.width)
+        assert s.budget > 1                            # the bound leaves room to search
+    finally:
+        fork.close()

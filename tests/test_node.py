@@ -647,3 +647,51 @@ def test_failure_reruns_delegated_half():
 
 def test_graceful_stop_hands_queue_to_neighbour():
     graceful_stop_scenario(OracleEngine(), OracleEngine())
+
+
+# ------------------------------------------------ every GPU of the box (north_star: sharding, N3)
+def test_node_on_multi_device_engine():
+    """A SudokuNode on a 3-device MultiDeviceEngine (oracle doubles): batches and the continued
+    search of a budget-hit board are sharded over the devices, and the answers are the reference's:
+    the wiki puzzle, DEMO8's golden lex-first board (a budget-hit, continued search) and the
+    documented 504 "exhausted" for '55'+79 zeros."""
+    import threading
+    from distributed_sudoku_solver_amd.shard import MultiDeviceEngine
+    devs = [_TinyBudget() for _ in range(3)]
+    mde = MultiDeviceEngine(devs)
+    node = SudokuNode("127.0.0.1", 0, 0, engine=mde, delay_ms=0, node_budget=1, search_width=8,
+                      search_max_pending=20_000, search_limit_s=3.0).start()
+    try:
+        assert node.search_engine is mde                      # doubles cannot fork: shared
+        code, body = _post(node.http_port, _grid(synth.WIKI))
+        assert code == 201 and "".join(str(v) for row in body["solution"] for v in row) == synth.WIKI_SOLUTION
+        code, body = _post(node.http_port, _grid(DEMO8))
+        assert code == 201 and "".join(str(v) for row in body["solution"] for v in row) == DEMO8_FIRST
+        res = {}
+        th = threading.Thread(target=lambda: res.__setitem__("c", _post_any(node.http_port, _grid(CONFLICT55))))
+        th.start()
+        th.join(60)
+        code, body = res["c"]
+        assert code == 504 and body["exhausted"] is True and body["solution"] is None
+        # the continued searches' launches used every device (width 8 per device: 24 sub-boards a slice)
+        assert all(len(d.batches) > 3 for d in devs), [d.batches for d in devs]
+        assert sum(d.expansions for d in devs) > 0
+    finally:
+        _stop([node])
+
+
+def test_multi_device_expand_is_an_ordered_partition():
+    """MultiDeviceEngine.expand splits the parents contiguously over the devices and concatenates
+    the children in order: solving them in order gives the parents' completions in lex order."""
+    from distributed_sudoku_solver_amd.shard import MultiDeviceEngine
+    from oracle import oracle as O
+    mde = MultiDeviceEngine([OracleEngine() for _ in range(3)])
+    b = synth.parse(DEMO8)
+    kids = mde.expand(np.stack([b, b, b, b]), None, target=40)
+    one = naive_expand(b[None], None, target=10)
+    assert len(kids) >= 40
+    out, st, _ = O.naive_solve_batch(kids, budget=10_000_000, threads=2)
+    sols = ["".join(map(str, o)) for o, s_ in zip(out, st) if s_ == 1]
+    ref_out, ref_st, _ = O.naive_solve_batch(one, budget=10_000_000, threads=2)
+    ref = ["".join(map(str, o)) for o, s_ in zip(ref_out, ref_st) if s_ == 1]
+    assert sols[0] == DEMO8_FIRST and sorted(set(sols)) == sorted(set(ref))

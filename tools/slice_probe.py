@@ -1,8 +1,11 @@
 """Wall time of search.LexSearch slices on the GPU (dev tool): the conflict board '55'+79 zeros
-(unrefutable by propagation) and a few hard boards, per slice: budget, launch + expansion time,
-worklist size.  Sizes the node's slice_target_s / node_budget (node.py).
+(unrefutable by propagation), per slice: budget, width, the slice's time split into the launch
+(engine.solve_batch: H2D + kernel + D2H), the expansion (engine.expand) and the host work around
+them, and the worklist size.  Sizes the node's slice_target_s / node_budget (node.py).
 
-    python tools/slice_probe.py [--slices 12] [--target 0.01]
+    python tools/slice_probe.py [--slices 12] [--target 0.01] [--node]
+
+--node: the search exactly as a SudokuNode continues a budget-hit board (node.py _run_batch).
 """
 import argparse
 import os
@@ -16,25 +19,70 @@ from distributed_sudoku_solver_amd import SudokuEngine  # noqa: E402
 from distributed_sudoku_solver_amd.search import LexSearch, default_budget  # noqa: E402
 
 
+class _Timed:
+    """Engine proxy that adds up the wall time of solve_batch and expand calls."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.t_solve = self.t_expand = 0.0
+        self.n_solve = self.n_expand = 0
+
+    def solve_batch(self, *a, **k):
+        t0 = time.perf_counter()
+        try:
+            return self.eng.solve_batch(*a, **k)
+        finally:
+            self.t_solve += time.perf_counter() - t0
+            self.n_solve += len(a[0])
+
+    def expand(self, *a, **k):
+        t0 = time.perf_counter()
+        try:
+            r = self.eng.expand(*a, **k)
+            self.n_expand += len(r)
+            return r
+        finally:
+            self.t_expand += time.perf_counter() - t0
+
+    def __getattr__(self, k):
+        return getattr(self.eng, k)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--slices", type=int, default=12)
     ap.add_argument("--target", type=float, default=0.01)
+    ap.add_argument("--node", action="store_true", help="only the node's configuration")
     args = ap.parse_args()
     board = np.zeros(81, np.uint8)
     board[0] = board[1] = 5
+    worst = {}
     with SudokuEngine(0) as eng:
         b0 = default_budget(eng)
-        for target in (None, args.target):
-            s = LexSearch(eng, board, budget=b0, hit=True, slice_target_s=target)
+        configs = [("node", args.target)] if args.node else [("free", None), ("node", args.target)]
+        for name, target in configs:
+            te = _Timed(eng)
+            if name == "node":
+                s = LexSearch.for_node(te, board, None, slice_target_s=target)
+            else:
+                s = LexSearch(te, board, budget=b0, hit=True, slice_target_s=target)
+            worst[name] = 0.0
             for k in range(args.slices):
-                t0 = time.monotonic()
+                te.t_solve = te.t_expand = 0.0
+                te.n_solve = te.n_expand = 0
+                t0 = time.perf_counter()
                 done = s.step()
-                dt = time.monotonic() - t0
-                print(f"target={target} slice={k} budget={s.budget} pending={s.pending} "
-                      f"nodes={s.nodes} ms={1e3 * dt:.2f} done={done}", flush=True)
+                dt = time.perf_counter() - t0
+                worst[name] = max(worst[name], dt)
+                print(f"{name} target={target} slice={k} budget={s.budget} width={te.n_solve} pending={s.pending} "
+                      f"nodes={s.nodes} ms={1e3 * dt:.2f} launch_ms={1e3 * te.t_solve:.2f} "
+                      f"expand_ms={1e3 * te.t_expand:.2f} (kids {te.n_expand}) "
+                      f"host_ms={1e3 * (dt - te.t_solve - te.t_expand):.2f} "
+                      f"rate_est={getattr(s, 'rate', 0.0):.3g} done={done}", flush=True)
                 if done:
                     break
+    for name, w in worst.items():
+        print(f"worst slice {name}: {1e3 * w:.2f} ms", flush=True)
 
 
 if __name__ == "__main__":

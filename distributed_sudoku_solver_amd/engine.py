@@ -294,6 +294,18 @@ class SudokuEngine:
                 "sdk_frontier_boards_dev")
         return p.value, size.value
 
+    def frontier_records(self, lo, hi):
+        """(device address, bytes) of records [lo, hi) of the current frontier: what a rank sends
+        to another (comm p2p) when it hands on part of its live subtrees."""
+        p, size = self.frontier_boards()
+        if not 0 <= lo <= hi <= size:
+            raise ValueError(f"records [{lo}, {hi}) outside the frontier of {size}")
+        return p + 81 * int(lo), 81 * (int(hi) - int(lo))
+
+    def record_buffer(self, n):
+        """A device buffer for n board records (a receive buffer of moved records)."""
+        return self.alloc(81 * max(1, int(n)))
+
     def frontier_load(self, d_boards, n, offset=0):
         """The n records at device buffer `d_boards` (+ offset boards) become the current
         count-mode frontier."""

@@ -175,6 +175,29 @@ class TcpComm:
         parts = self.allgather_bytes(send.view(np.uint8)[:nbytes].tobytes())
         recv.view(np.uint8)[:self.world * nbytes] = np.frombuffer(b"".join(parts), dtype=np.uint8)
 
+    def p2p(self, ops):
+        """Point-to-point as shard.RcclComm.p2p (host arrays).  A star cannot connect two
+        non-root ranks directly, so this is a collective here: every rank calls it (with its own
+        ops, possibly none), the messages travel through one allgather, and each rank keeps the
+        ones addressed to it."""
+        out = b"".join(struct.pack("<iiQ", self.rank, int(peer), int(nbytes)) +
+                       np.ascontiguousarray(buf).view(np.uint8).reshape(-1)[:nbytes].tobytes()
+                       for kind, peer, buf, nbytes in ops if kind == 0 and nbytes)
+        want = {int(peer): (buf, int(nbytes)) for kind, peer, buf, nbytes in ops if kind == 1 and nbytes}
+        for blob in self.allgather_bytes(out):
+            off = 0
+            while off < len(blob):
+                src, dst, n = struct.unpack_from("<iiQ", blob, off)
+                off += 16
+                if dst == self.rank and src in want:
+                    buf, nb = want.pop(src)
+                    if nb != n:
+                        raise ValueError(f"p2p size mismatch from rank {src}: {n} != {nb}")
+                    buf.view(np.uint8).reshape(-1)[:n] = np.frombuffer(blob, np.uint8, n, off)
+                off += n
+        if want:
+            raise ConnectionError(f"p2p: nothing arrived from ranks {sorted(want)}")
+
     def gather(self, local, root=0):
         """Row-concatenation of every rank's array at `root` (None elsewhere)."""
         local = np.ascontiguousarray(local)

@@ -312,6 +312,11 @@ class RcclComm:
     def allgather(self, send, recv, nbytes):
         self.engine.comm_allgather(send, recv, nbytes)
 
+    def p2p(self, ops):
+        """Grouped ncclSend / ncclRecv on device memory: ops = [(L.SDK_COMM_SEND | RECV, peer,
+        device buffer or address, nbytes)]; a rank without ops need not call."""
+        self.engine.comm_p2p(ops)
+
     def close(self):
         self.engine.comm_destroy()
 
@@ -347,6 +352,26 @@ class HostComm:
         parts = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(parts, t, group=self.group)
         recv.view(np.uint8)[:self.world * nbytes] = torch.cat(parts).numpy()
+
+    def p2p(self, ops):
+        """Point-to-point over the group (gloo isend / irecv): ops as RcclComm.p2p, host arrays."""
+        import torch
+        import torch.distributed as dist
+        reqs, recvs = [], []
+        for kind, peer, buf, nbytes in ops:
+            if not nbytes:
+                continue
+            if kind == L.SDK_COMM_SEND:
+                t = torch.from_numpy(np.ascontiguousarray(buf).view(np.uint8).reshape(-1)[:nbytes].copy())
+                reqs.append(dist.isend(t, dst=int(peer), group=self.group))
+            else:
+                t = torch.empty(int(nbytes), dtype=torch.uint8)
+                reqs.append(dist.irecv(t, src=int(peer), group=self.group))
+                recvs.append((buf, t))
+        for r in reqs:
+            r.wait()
+        for buf, t in recvs:
+            buf.view(np.uint8).reshape(-1)[:t.numel()] = t.numpy()
 
     def broadcast_bytes(self, data, root=0):
         import torch
@@ -521,36 +546,128 @@ def rebalance_ranges(ranges, min_split=2):
     return R
 
 
-def sharded_count_rebalanced(engine, board, rank, world, limit=0, comm=None, target=None, chunk=None, info=None,
-                             ranges=None):
-    """sharded_count with dynamic rebalancing of the replicated frontier.
+def rebalance_plan(states, min_split=2):
+    """One rebalancing step over the all-gathered rank states (lo, hi, local): `local` = the
+    rank's frontier is no longer the replicated one (it received or refined records).
 
-    Each rank starts on a contiguous block of the frontier and counts it `chunk` boards per round.
-    After every round the ranks all-gather their live ranges (RCCL ncclAllGather of 2 x int64 per
-    rank on device memory, or gloo in the CPU tests) and ranks that ran dry take the upper half of
-    the largest remaining range (rebalance_ranges).  Subtree sizes are heavy-tailed, so a static split
-    leaves GPUs idle behind the rank holding the heavy boards; here they finish within about one
-    round of each other.  Counts are combined by one all-reduce(sum) at the end.
-    `ranges` (optional, one (lo, hi) per rank, same on every rank) replaces the initial equal blocks,
-    e.g. to resume a partial count.
-    Returns (total, status, frontier_size) like sharded_count; `info` (dict) gets rounds/steals."""
+    Returns (new_states, moves, refines), a pure function of the gathered values (every rank
+    computes the same):
+      * in rank order, a rank with an empty range takes the upper half [mid, hi) of the largest
+        remaining range (ties -> lowest rank; not below `min_split` boards; a rank that takes
+        records this step gives none).  moves = [(donor, receiver, mid, hi, by_records)]:
+        by_records when either frontier is not the replicated one -- the donor then sends the
+        board records (81 B each) of [mid, hi) and the receiver's frontier becomes them;
+        otherwise only the range travels;
+      * if a rank is still empty after that, every rank whose remaining boards are too few to
+        split refines them into their second-level children (refines = [rank]): the next step
+        splits those records -- the device form of the reference handing on a partial board
+        mid-search (DHT_Node.py:502-509), here for a subtree too heavy to leave on one GPU."""
+    S = [[int(a), int(b), int(c)] for a, b, c in states]
+    moves, takers = [], set()
+    split = max(2, min_split)
+    for r in range(len(S)):
+        if S[r][1] > S[r][0]:
+            continue
+        cands = [k for k in range(len(S)) if k not in takers and k != r]
+        if not cands:
+            continue
+        donor = max(cands, key=lambda k: (S[k][1] - S[k][0], -k))
+        rem = S[donor][1] - S[donor][0]
+        if rem < split:
+            continue
+        mid = S[donor][0] + rem // 2
+        end = S[donor][1]
+        by_records = bool(S[donor][2] or S[r][2])
+        moves.append((donor, r, mid, end, by_records))
+        S[r] = [0, end - mid, 1] if by_records else [mid, end, S[r][2]]
+        S[donor][1] = mid
+        takers.add(r)
+    refines = []
+    if any(b <= a for a, b, _ in S):
+        refines = [k for k in range(len(S)) if 0 < S[k][1] - S[k][0] < split and k not in takers]
+    return S, moves, refines
+
+
+def refine_target(world, min_split):
+    """Boards a rank's refined subtree should come to: enough to give every rank a split."""
+    return max(4 * world, 2 * max(2, min_split))
+
+
+def sharded_count_rebalanced(engine, board, rank, world, limit=0, comm=None, target=None, chunk=None, info=None,
+                             ranges=None, move_records=True):
+    """sharded_count with dynamic rebalancing.
+
+    Each rank starts on a contiguous block of the replicated frontier (or on `ranges`, one
+    (lo, hi) per rank, the same on every rank) and counts it `chunk` boards per round.  Before
+    every round the ranks all-gather their state (lo, hi, local: RCCL ncclAllGather of 3 x int64
+    per rank on device memory, or gloo / TcpComm in the CPU tests) and rebalance_plan moves work
+    to ranks that ran dry: the upper half of the largest live range -- as an index range while
+    both frontiers are the replicated one, else as board records sent with grouped
+    ncclSend/ncclRecv (comm.p2p) straight from the donor's frontier into the receiver's.  A
+    rank left with too few boards to split while another is dry refines them into their
+    second-level children first (engine.frontier_refine_range) and skips that round's count, so
+    the next round can hand half of them on: one heavy subtree does not stay on one GPU.
+    Counts (with the completions each rank met while refining) are combined by one
+    all-reduce(sum) at the end.  move_records=False keeps round 3's index-only rebalancing.
+    Returns (total, status, frontier_size) like sharded_count; `info` (dict) gets rounds,
+    steals, moved records and refinements."""
     if world > 1 and comm is None:
         raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
     size, leaves = engine.frontier_build(board, mode=L.SDK_FRONTIER_COUNT,
                                          target=count_target(engine, world) if target is None else target)
     if chunk is None:   # one launch when there is no one to rebalance with; else 2 boards per resident wave
         chunk = max(1, size) if comm is None else max(1, default_target(engine, 1) // 4)
+    min_split = max(2, chunk // 2)
     lo, hi = shard_bounds(size, rank, world) if ranges is None else (int(ranges[rank][0]), int(ranges[rank][1]))
     lo, hi = min(lo, size), min(hi, size)
+    local = 0
     res = engine.result_buffer(2, np.uint64)
-    mine = engine.result_buffer(2, np.int64)
-    allr = engine.result_buffer(2 * world, np.int64)
+    mine = engine.result_buffer(3, np.int64)
+    allr = engine.result_buffer(3 * world, np.int64)
     tot = engine.result_buffer(2, np.uint64)
-    count = hits = rounds = steals = 0
+    inbox = None                                         # receive buffer of moved records (grown as needed)
+    count = hits = rounds = steals = moved = refined = 0
+    own_leaves = 0
     try:
         while True:
+            skip = False
+            if comm is not None:
+                _store(mine, [lo, hi, local], np.int64)
+                comm.allgather(mine, allr, 24)
+                S = engine.read(allr, 3 * world, np.int64).reshape(world, 3)
+                if all(b <= a for a, b, _ in S):
+                    break
+                if move_records:
+                    newS, moves, refines = rebalance_plan(S, min_split=min_split)
+                else:
+                    newR = rebalance_ranges(S[:, :2], min_split=min_split)
+                    newS = [[a, b, 0] for a, b in newR]
+                    moves, refines = [], []
+                steals += sum(1 for a, b in zip(S.tolist(), newS) if a[:2] != b[:2] and a[1] <= a[0])
+                ops, got = [], None
+                for donor, recv, mid, end, by_records in moves:
+                    if not by_records:
+                        continue
+                    moved += end - mid
+                    if rank == donor:
+                        ops.append((L.SDK_COMM_SEND, recv) + engine.frontier_records(mid, end))
+                    elif rank == recv:
+                        inbox = _grow_records(engine, inbox, end - mid)
+                        ops.append((L.SDK_COMM_RECV, donor, inbox, 81 * (end - mid)))
+                        got = end - mid
+                if any(m[4] for m in moves):
+                    comm.p2p(ops)                         # every rank: a collective on host transports
+                if got is not None:
+                    engine.frontier_load(inbox, got)
+                lo, hi, local = (int(v) for v in newS[rank])
+                if rank in refines:
+                    n_kids, lv = engine.frontier_refine_range(lo, hi, refine_target(world, min_split))
+                    own_leaves += lv
+                    lo, hi, local = 0, n_kids, 1
+                    refined += 1
+                    skip = True
             end = min(hi, lo + chunk)
-            if end > lo:
+            if end > lo and not skip:
                 engine.frontier_count(lo, 1, end, limit, res)
                 c, h = (int(x) for x in engine.read(res, 2, np.uint64))
                 count += c
@@ -559,30 +676,31 @@ def sharded_count_rebalanced(engine, board, rank, world, limit=0, comm=None, tar
                 if limit and count >= limit:
                     lo = hi                                    # this rank alone reached the limit
             rounds += 1
-            if comm is None:                                   # single rank, nothing to exchange
-                if lo >= hi:
-                    break
-                continue
-            _store(mine, [lo, hi], np.int64)
-            comm.allgather(mine, allr, 16)
-            R = engine.read(allr, 2 * world, np.int64).reshape(world, 2)
-            if all(b <= a for a, b in R):
+            if comm is None and lo >= hi:                     # single rank, nothing to exchange
                 break
-            newR = rebalance_ranges(R, min_split=max(2, chunk // 2))
-            steals += sum(1 for a, b in zip(R.tolist(), newR) if a != b and a[1] <= a[0])
-            lo, hi = newR[rank]
-        _store(tot, [count, hits], np.uint64)
+        _store(tot, [count + own_leaves, hits], np.uint64)
         if comm is not None:
             comm.allreduce(tot, 2, np.uint64, "sum")
         count, hits = (int(x) for x in engine.read(tot, 2, np.uint64))
     finally:
-        for h in (res, mine, allr, tot):
+        for h in (res, mine, allr, tot, inbox):
             if hasattr(h, "free"):
                 h.free()
     if info is not None:
-        info.update(rounds=rounds, steals=steals, chunk=chunk)
+        info.update(rounds=rounds, steals=steals, chunk=chunk, moved_records=moved, refines=refined)
     total = count + leaves
     if limit and total > limit:
         total = limit
     st = -2 if hits else (1 if total > 0 else 0)
     return total, st, size
+
+
+def _grow_records(engine, buf, n):
+    """A receive buffer for n board records (the engine's: a DeviceBuffer, or a host array)."""
+    need = 81 * max(1, int(n))
+    have = (buf.nbytes if hasattr(buf, "nbytes") else 0) if buf is not None else 0
+    if buf is not None and have >= need:
+        return buf
+    if buf is not None and hasattr(buf, "free"):
+        buf.free()
+    return engine.record_buffer(max(need, 2 * have) // 81)

@@ -93,6 +93,24 @@ class OracleEngine:
         self.frontier = self._expand(list(self.frontier[first::step]), target, None)
         return len(self.frontier), 0
 
+    def frontier_refine_range(self, lo, hi, target):
+        """Boards [lo, hi) of the frontier, expanded on until >= target (no leaves dropped here)."""
+        self.calls.append(("refine_range", lo, hi, len(self.frontier)))
+        self.frontier = self._expand(list(self.frontier[lo:hi]), target, None)
+        return len(self.frontier), 0
+
+    def frontier_records(self, lo, hi):
+        recs = np.stack(self.frontier[lo:hi]).reshape(-1) if hi > lo else np.zeros(0, np.uint8)
+        return recs, 81 * (hi - lo)
+
+    def record_buffer(self, n):
+        return np.zeros(81 * max(1, int(n)), np.uint8)
+
+    def frontier_load(self, buf, n, offset=0):
+        self.calls.append(("load", n))
+        raw = np.asarray(buf).view(np.uint8).reshape(-1)[81 * offset: 81 * (offset + n)]
+        self.frontier = [r.copy() for r in raw.reshape(-1, 81)]
+
     @staticmethod
     def _expand(fr, target, allowed0):
         while fr and len(fr) < max(target, 1):
@@ -216,6 +234,9 @@ class BenchStubEngine(OracleEngine):
 
     def comm_allgather(self, send, recv, nbytes):
         self._comm.allgather(send, recv, nbytes)
+
+    def comm_p2p(self, ops):
+        self._comm.p2p([(k, p, b.data if hasattr(b, "data") else b, n) for k, p, b, n in ops])
 
     def alloc(self, nbytes):
         return _HostBuffer(nbytes)

@@ -63,9 +63,20 @@ def _worker(rank, world, port, q):
         info = {}
         b16 = synth.parse(s1[:-9] + "000800000")
         total, st, size = sharded_count_rebalanced(eng, b16, rank, world, comm=comm, chunk=2, info=info,
-                                                   ranges=[(0, 10 ** 9), (0, 0)])
+                                                   ranges=[(0, 10 ** 9), (0, 0)], move_records=False)
         idx = sorted(i for c in eng.calls if c[0] == "count" for i in c[1])
         q.put(("rebal", rank, total == 7309 and st == 1, idx, size, info["steals"]))
+        # record moves: rank 0 holds ONE heavy board (the whole 16-clue board, a
+        # one-board frontier), rank 1 nothing.  Rank 0 refines it into second-level records, sends
+        # half of them to rank 1 (p2p), and rank 1 counts part of that board's subtree
+        eng.calls = []
+        info = {}
+        total, st, size = sharded_count_rebalanced(eng, b16, rank, world, comm=comm, chunk=2, info=info, target=1,
+                                                   ranges=[(0, 1), (1, 1)])
+        loads = [c[1] for c in eng.calls if c[0] == "load"]
+        counted = sum(len(c[1]) for c in eng.calls if c[0] == "count")
+        q.put(("records", rank, total == 7309 and st == 1, size, loads, counted, info["refines"],
+               info["moved_records"]))
         # first solution of the multi-solution demo board (sudoku.py:99-109) = reference golden
         demo = synth.parse("000100000000320000000009000000000070000000000000900000000000900000000003000000000")
         golden = "234156789179328456568479132391245678425687391687913245752831964816794523943562817"
@@ -105,9 +116,14 @@ def test_world2_gloo_gather():
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    got = [q.get(timeout=5) for _ in range(3 + 7 * world)]
+    got = [q.get(timeout=5) for _ in range(3 + 8 * world)]
     res = {g[0]: g[1:] for g in got if g[0] not in ("calls", "count_split", "count_refine", "first", "first_range", "unsolvable",
-                                                    "rebal")}
+                                                    "rebal", "records")}
+    rec = {g[1]: g[2:] for g in got if g[0] == "records"}
+    assert rec[0][0] and rec[1][0], rec                                   # exact total (7,309) on both ranks
+    assert rec[0][1] == 1                                                  # a one-board frontier
+    assert rec[0][4] >= 1 and rec[0][5] > 0                                # rank 0 refined, records moved
+    assert rec[1][2] and rec[1][3] > 0, rec                                # rank 1 loaded records and counted
     rebal = {g[1]: g[2:] for g in got if g[0] == "rebal"}
     assert rebal[0][0] and rebal[1][0]                                      # same total on both ranks
     fsize = rebal[0][2]

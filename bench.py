@@ -81,6 +81,7 @@ def parse_args():
     ap.add_argument("--hard-leg", type=int, default=1,
                     help="hard-search leg: the committed hard set (100k distinct puzzles that search) and its "
                          "1000 heaviest, one launch vs the phased solve with subtree donation (0 = skip)")
+    ap.add_argument("--hard-reps", type=int, default=10, help="hard_1m: symmetries of the 100k hard set per GPU")
     ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
     ap.add_argument("--c5-boards", default="15,14",
                     help="C5 boards: 16/15/14 clues (S1 with clues removed; counts 7,309 / 3,481,026 / 18,204,270); "
@@ -438,21 +439,37 @@ def hard_leg(eng, d, args, synth, L):
         p, s = synth.apply_symmetries(p, g, rl), synth.apply_symmetries(s, g, rl)
         g, rl = synth.random_symmetries(rng, len(hp))
         hp, hs = synth.apply_symmetries(hp, g, rl), synth.apply_symmetries(hs, g, rl)
-    res, bad = {}, 0
-    for name, (bp, bs) in (("hard_100k", (p, s)), ("heaviest_1000", (hp, hs))):
+    # hard_1m: the 100k set x 10 seeded symmetries (a throughput-bound batch that searches,
+    # VERDICT r3 item 5); symmetries keep every board's solution count and its search shape
+    rng = np.random.default_rng([args.seed, d.rank, 7])
+    reps = max(1, args.hard_reps)
+    mp, ms = [p], [s]
+    for _ in range(reps - 1):
+        g, rl = synth.random_symmetries(rng, len(p))
+        mp.append(synth.apply_symmetries(p, g, rl))
+        ms.append(synth.apply_symmetries(s, g, rl))
+    mp, ms = np.concatenate(mp), np.concatenate(ms)
+    res, bad, checked = {}, 0, 0
+    old_max = eng.get_option(L.SDK_OPT_DONATE_MAX)
+    for name, (bp, bs) in (("hard_100k", (p, s)), ("heaviest_1000", (hp, hs)), ("hard_1m", (mp, ms))):
         legs = {}
         for mode, dn in (("one_launch", 0), ("donation", 16 if name == "heaviest_1000" else 1)):
             eng.set_option(L.SDK_OPT_DONATE, dn)
+            eng.set_option(L.SDK_OPT_DONATE_MAX, 0)       # phased at any size (hard_1m is above the default)
             el, b = _timed_solves(eng, d, bp, bs, 5)
             bad += b
+            checked += d.world * len(bp)
             legs[mode] = {"value": d.world * len(bp) / el, "unit": "puzzles/s", "ms": el * 1000.0,
                           "split_budget": dn if dn > 1 else (128 if dn else None),
                           "split_boards": eng.get_option(L.SDK_OPT_SPLIT_BOARDS),
                           "lex_boards": eng.get_option(L.SDK_OPT_LEX_BOARDS),
                           "donated": eng.get_option(L.SDK_OPT_DONATED)}
         eng.set_option(L.SDK_OPT_DONATE, 1)
+        eng.set_option(L.SDK_OPT_DONATE_MAX, old_max)
         legs["donation_speedup"] = legs["donation"]["value"] / legs["one_launch"]["value"]
         res[name] = legs
+    res["hard_1m"]["workload"] = f"the {len(p)} hard puzzles x {reps} seeded symmetries ({len(mp)} boards) per GPU"
+    res["hard_1m"]["roofline"] = pmc_record(args.pmc_summary, "hard_1m", len(mp))
     stats = {}
     eng.set_option(L.SDK_OPT_DONATE, 0)     # per-board work of one slot per board
     for kind, nm in ((L.SDK_WORK_NODES, "nodes"), (L.SDK_WORK_ROUNDS, "rounds"), (L.SDK_WORK_DEPTH, "depth")):
@@ -465,7 +482,7 @@ def hard_leg(eng, d, args, synth, L):
     res["workload"] = (f"{len(p)} distinct hard puzzles per GPU ({int((p > 0).sum(1).mean())} clues on average, "
                        f"committed set) and their 1000 heaviest, resident in HBM")
     res["search"] = stats
-    res["parity"] = {"mismatched_boards": bad, "checked_boards": d.world * 5 * 2 * (len(p) + len(hp))}
+    res["parity"] = {"mismatched_boards": bad, "checked_boards": 5 * checked}
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
         res["cpu_baseline_c_port"] = cpu_baseline_c(p, min(args.cpu_seconds, 5.0), cpu_share())
     return res

@@ -1,6 +1,8 @@
 """expand4_kernel (four boards per wave, solve4's round) builds the same frontier, byte for byte,
 as expand_kernel (one board per wave): first-solution frontiers compared board by board, count
 frontiers by size, leaves and the counts below them (the oracle's counter)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -62,3 +64,56 @@ def test_count_mode_frontier_identical(engine):
     for b in boards[3:]:
         assert engine.count_solutions(b)[0] == O.count(b, 0, 1)
     assert engine.count_solutions(boards[1]) == (3481026, 1)
+
+
+def _count(e, lo, hi):
+    res = e.result_buffer(2, np.uint64)
+    try:
+        e.frontier_count(lo, 1, hi, 0, res)
+        c, h = (int(x) for x in e.read(res, 2, np.uint64))
+    finally:
+        res.free()
+    assert h == 0
+    return c
+
+
+def test_frontier_records_move_and_refine(engine):
+    """The device primitives of the record-moving rebalance (shard.sharded_count_rebalanced):
+    records [mid, size) of one context's frontier, loaded into another context's frontier
+    straight from device memory (what ncclSend/ncclRecv move between ranks), count what they
+    counted in place; a range refined into second-level records keeps its count (15-clue C5
+    board, 3,481,026 completions in all)."""
+    s1 = synth.SEEDS17["S1"]
+    b15 = synth.parse(s1[:-9] + "0" * 9)
+    a, b = engine.fork(), engine.fork()
+    try:
+        size, leaves = a.frontier_build(b15, mode=L.SDK_FRONTIER_COUNT, target=4096)
+        assert size >= 4096
+        mid = size // 3
+        whole = _count(a, 0, size)
+        assert whole + leaves == 3481026
+        ptr, nbytes = a.frontier_records(mid, size)
+        assert nbytes == 81 * (size - mid)
+        b.frontier_load(ptr, size - mid)
+        assert b.frontier_boards()[1] == size - mid
+        assert _count(a, 0, mid) + _count(b, 0, size - mid) == whole
+        # one board's subtree, refined into its second-level records: same count
+        one = _count(a, 7, 8)
+        k, lv = a.frontier_refine_range(7, 8, 64)
+        assert k >= 2 and _count(a, 0, k) + lv == one
+        # records from a DeviceBuffer (a receive buffer), and a range of the context's own frontier
+        buf = b.record_buffer(5)
+        ptr, nbytes = b.frontier_records(0, 5)
+        host = np.empty(nbytes, np.uint8)
+        L.check(b.lib.sdk_memcpy_d2h(b.ctx, host.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr), nbytes))
+        buf.upload(host)
+        first5 = sum(_count(b, i, i + 1) for i in range(5))
+        a.frontier_load(buf, 5)
+        assert _count(a, 0, 5) == first5
+        p, n = b.frontier_boards()
+        b.frontier_load(p + 81 * 2, 3)                   # overlapping: staged through the second buffer
+        assert _count(b, 0, 3) == sum(_count(a, i, i + 1) for i in range(2, 5))
+        buf.free()
+    finally:
+        a.close()
+        b.close()

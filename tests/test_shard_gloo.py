@@ -171,3 +171,34 @@ def test_rebalance_ranges():
         before = sorted(i for a, b in R for i in range(a, b))
         after = sorted(i for a, b in N for i in range(a, b))
         assert before == after
+
+
+def test_rebalance_plan():
+    from distributed_sudoku_solver_amd.shard import rebalance_plan
+    # replicated frontiers on both sides: an index move, no records
+    S, moves, ref = rebalance_plan([[0, 100, 0], [5, 5, 0]])
+    assert S == [[0, 50, 0], [50, 100, 0]] and moves == [(0, 1, 50, 100, False)] and ref == []
+    # a donor that holds its own records: they travel, the receiver's frontier becomes them
+    S, moves, ref = rebalance_plan([[3, 11, 1], [5, 5, 0]])
+    assert S == [[3, 7, 1], [0, 4, 1]] and moves == [(0, 1, 7, 11, True)] and ref == []
+    # one board left, a rank dry: the holder refines (no move this step)
+    S, moves, ref = rebalance_plan([[0, 1, 0], [1, 1, 0], [4, 4, 0]])
+    assert moves == [] and ref == [0] and S[0] == [0, 1, 0]
+    # a rank that takes records this step does not give any
+    S, moves, ref = rebalance_plan([[0, 0, 0], [0, 0, 0], [0, 64, 1]])
+    assert [m[:2] for m in moves] == [(2, 0), (2, 1)]
+    assert S == [[0, 32, 1], [0, 16, 1], [0, 16, 1]]
+    # all done: nothing to do
+    assert rebalance_plan([[1, 1, 0], [2, 2, 1]]) == ([[1, 1, 0], [2, 2, 1]], [], [])
+    rng = np.random.default_rng(1)
+    for _ in range(300):                            # conservation: live boards are only re-partitioned
+        w = int(rng.integers(1, 9))
+        st = []
+        for _ in range(w):
+            lo = int(rng.integers(0, 100))
+            st.append([lo, lo + int(rng.integers(0, 40)) * int(rng.integers(0, 2)), int(rng.integers(0, 2))])
+        S, moves, ref = rebalance_plan(st, min_split=int(rng.integers(2, 6)))
+        assert sum(b - a for a, b, _ in S) == sum(b - a for a, b, _ in st)
+        recv = [m[1] for m in moves]
+        assert len(recv) == len(set(recv)) and not set(recv) & {m[0] for m in moves}
+        assert all(st[m[1]][1] <= st[m[1]][0] for m in moves)              # only dry ranks receive

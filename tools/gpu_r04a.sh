@@ -6,6 +6,7 @@ out=gpurun_out/r04a
 mkdir -p $out
 export TMPDIR=/tmp
 T="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+(cd /tmp && timeout -k 5 60 rocprofv3 --list-avail > $OLDPWD/$out/list_avail.txt 2>&1) || echo "list-avail failed"
 timeout -k 10 400 $T tests/test_gpu_donate.py > $out/donate.log 2>&1 || { tail -30 $out/donate.log; exit 1; }
 tail -2 $out/donate.log
 timeout -k 10 120 python -u tools/slice_probe.py --slices 30 > $out/slice_probe.log 2>&1 || { tail -30 $out/slice_probe.log; exit 1; }

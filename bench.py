@@ -441,14 +441,12 @@ def hard_leg(eng, d, args, synth, L):
         hp, hs = synth.apply_symmetries(hp, g, rl), synth.apply_symmetries(hs, g, rl)
     # hard_1m: the 100k set x 10 seeded symmetries (a throughput-bound batch that searches,
     # VERDICT r3 item 5); symmetries keep every board's solution count and its search shape
-    rng = np.random.default_rng([args.seed, d.rank, 7])
+    # (synth.make_hard_sym: the same boards tools/pmc_r04.sh profiles; rank r > 0 a symmetry of each)
     reps = max(1, args.hard_reps)
-    mp, ms = [p], [s]
-    for _ in range(reps - 1):
-        g, rl = synth.random_symmetries(rng, len(p))
-        mp.append(synth.apply_symmetries(p, g, rl))
-        ms.append(synth.apply_symmetries(s, g, rl))
-    mp, ms = np.concatenate(mp), np.concatenate(ms)
+    mp, ms = synth.make_hard_sym(len(p) * reps, threads=cpu_share())
+    if d.rank:
+        g, rl = synth.random_symmetries(np.random.default_rng([args.seed, d.rank, 7]), len(mp))
+        mp, ms = synth.apply_symmetries(mp, g, rl), synth.apply_symmetries(ms, g, rl)
     res, bad, checked = {}, 0, 0
     old_max = eng.get_option(L.SDK_OPT_DONATE_MAX)
     for name, (bp, bs) in (("hard_100k", (p, s)), ("heaviest_1000", (hp, hs)), ("hard_1m", (mp, ms))):

@@ -66,6 +66,12 @@ namespace sdk {
 #ifndef SDK_SOLVE4_WAVES_PER_EU
 #define SDK_SOLVE4_WAVES_PER_EU 7
 #endif
+// Measurement build only (tools/build_variant.sh noout -DSDK_SOLVE4_NO_OUTPUT=1): no board is
+// written (statuses still are) -- the A/B that prices the solver's whole output write, and so
+// an upper bound of what its extra write sectors cost (solver traffic)
+#ifndef SDK_SOLVE4_NO_OUTPUT
+#define SDK_SOLVE4_NO_OUTPUT 0
+#endif
 // DFS levels kept in LDS (per level: 2 slots x 64 lanes x 8 B = 1 KiB; deeper levels go
 // to the per-workgroup global stack).  Default 0: a 17-clue board rarely branches, so the
 // stack is cold, and the 4.5 KiB block lets occupancy follow the VGPR budget: 7 waves per
@@ -1376,7 +1382,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
     uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
     if (a.count_mode && w.hl == 0 && st != -2 && b.count)
         atomicAdd(&s_count4, (unsigned long long)b.count);
-    if (st != 1 && w.act && a.out) {  // the reference restores the grid (DHT_Node.py:535)
+    if (st != 1 && w.act && a.out && !SDK_SOLVE4_NO_OUTPUT) {  // the reference restores the grid (DHT_Node.py:535)
         const uint8_t* sin = w.s_in + HI * 81;
         dst[w.c0] = sin[w.c0];
         dst[w.c0 + 27] = sin[w.c0 + 27];
@@ -1500,7 +1506,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
             }
             PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, 1));   // LEX: the region's first
             return;
-        } else if (b.count == 1 && w.act && a.out) {
+        } else if (b.count == 1 && w.act && a.out && !SDK_SOLVE4_NO_OUTPUT) {
             uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
             const uint8_t* sin = w.s_in + HI * 81;
             const uint32_t i0 = sin[w.c0], i1 = sin[w.c0 + 27], i2 = sin[w.c0 + 54];

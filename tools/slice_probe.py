@@ -8,6 +8,7 @@ them, and the worklist size.  Sizes the node's slice_target_s / node_budget (nod
 --node: the search exactly as a SudokuNode continues a budget-hit board (node.py _run_batch).
 """
 import argparse
+import gc
 import os
 import sys
 import time
@@ -48,16 +49,33 @@ class _Timed:
         return getattr(self.eng, k)
 
 
+def _throttled_us():
+    """cgroup v2 CPU throttling of this process's group (0 if not available)."""
+    for path, key, scale in (("/sys/fs/cgroup/cpu.stat", "throttled_usec", 1),
+                             ("/sys/fs/cgroup/cpu/cpu.stat", "throttled_time", 1e-3),
+                             ("/sys/fs/cgroup/cpu,cpuacct/cpu.stat", "throttled_time", 1e-3)):
+        try:
+            with open(path) as f:
+                for line in f:
+                    if line.startswith(key):
+                        return int(int(line.split()[1]) * scale)
+        except OSError:
+            continue
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--slices", type=int, default=12)
     ap.add_argument("--target", type=float, default=0.01)
     ap.add_argument("--node", action="store_true", help="only the node's configuration")
+    ap.add_argument("--fork", action="store_true", help="run on a forked context (as a node does)")
     args = ap.parse_args()
     board = np.zeros(81, np.uint8)
     board[0] = board[1] = 5
     worst = {}
-    with SudokuEngine(0) as eng:
+    with SudokuEngine(0) as eng0:
+        eng = eng0.fork() if args.fork else eng0
         b0 = default_budget(eng)
         configs = [("node", args.target)] if args.node else [("free", None), ("node", args.target)]
         for name, target in configs:
@@ -70,15 +88,19 @@ def main():
             for k in range(args.slices):
                 te.t_solve = te.t_expand = 0.0
                 te.n_solve = te.n_expand = 0
+                thr0, cpu0, gc0 = _throttled_us(), time.process_time(), sum(g["collections"] for g in gc.get_stats())
                 t0 = time.perf_counter()
                 done = s.step()
                 dt = time.perf_counter() - t0
+                thr = _throttled_us() - thr0
+                cpu = time.process_time() - cpu0
+                gcs = sum(g["collections"] for g in gc.get_stats()) - gc0
                 worst[name] = max(worst[name], dt)
                 print(f"{name} target={target} slice={k} budget={s.budget} width={te.n_solve} pending={s.pending} "
                       f"nodes={s.nodes} ms={1e3 * dt:.2f} launch_ms={1e3 * te.t_solve:.2f} "
                       f"expand_ms={1e3 * te.t_expand:.2f} (kids {te.n_expand}) "
                       f"host_ms={1e3 * (dt - te.t_solve - te.t_expand):.2f} "
-                      f"rate_est={getattr(s, 'rate', 0.0):.3g} done={done}", flush=True)
+                      f"cpu_ms={1e3 * cpu:.2f} throttled_ms={thr / 1e3:.2f} gc={gcs} done={done}", flush=True)
                 if done:
                     break
     for name, w in worst.items():

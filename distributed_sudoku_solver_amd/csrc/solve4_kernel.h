@@ -360,9 +360,75 @@ __device__ __forceinline__ void unit4(const uint2 (&v)[9], uint32_t E, uint32_t 
           [e] "v"(E), [dn] "v"(Dn));
 }
 
+// A board's statics (D, E of every unit) from its FIRST round instead of a pass of their own
+// (statics4: 3 stores, 9 unit reads and two wave barriers per board start).  A board that starts
+// carries E = kFresh4 in its half; a round of a wave with such a board reads the same nine cell
+// words a statics pass would -- at the first round a board's closed cells are exactly its givens --
+// and derives D and E from them (unit4f) before they are used.
+#ifndef SDK_SOLVE4_FRESH_ROUND
+#define SDK_SOLVE4_FRESH_ROUND 0
+#endif
+constexpr uint32_t kFresh4 = 0x8000u;                 // E of a board whose statics are pending
+// the plain kernel only: the donation kernel keeps statics4 (its 96-VGPR build spills a 64-bit
+// value to an odd register pair with unit4f, which the gfx950 backend rejects)
+constexpr bool kFresh4Round = SDK_SOLVE4_FRESH_ROUND != 0;
+
 #ifndef SDK_SOLVE4_SPLIT_READS
 #define SDK_SOLVE4_SPLIT_READS 1
 #endif
+
+// unit4 for a round of a wave where some board just started (its E half = kFresh4): that
+// board's statics come from the nine cells read here (its closed cells are its givens):
+//   dup = digits taken twice (given twice), inert = an out-of-domain given in the unit,
+//   E = 0x1FF if neither, D (as Dn = kC2 & ~dup); the other boards keep theirs.
+// Then once / T / bm as unit4 with the new statics.  E and Dn are rewritten in place.
+__device__ __forceinline__ void unit4f(const uint2 (&v)[9], uint32_t& E, uint32_t& Dn, uint32_t& once, uint32_t& T,
+                                       uint32_t& bm) {
+    // as many temporaries as unit4 (its register budget): t1..t3 are reused once twice(S) is
+    // formed (t1 = fresh mask, t2 = exact digits, t3 = dup), E and Dn are rewritten in place
+    uint32_t ox, os, t0, t1, t2, t3;
+    asm("v_or3_b32 %[ox], %[a0], %[a1], %[a2]\n\t"
+        "v_bitop3_b32 %[t0], %[a0], %[a1], %[a2] bitop3:0xe8\n\t"
+        "v_bitop3_b32 %[t1], %[ox], %[a3], %[a4] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a3], %[a4]\n\t"
+        "v_bitop3_b32 %[t2], %[ox], %[a5], %[a6] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a5], %[a6]\n\t"
+        "v_bitop3_b32 %[t3], %[ox], %[a7], %[a8] bitop3:0xe8\n\t"
+        "v_or3_b32 %[ox], %[ox], %[a7], %[a8]\n\t"
+        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        "v_bitop3_b32 %[once], %[ox], %[t0], %[t3] bitop3:0x10\n\t"   // candidates in exactly one cell
+        "v_or3_b32 %[os], %[b0], %[b1], %[b2]\n\t"
+        "v_bitop3_b32 %[t0], %[b0], %[b1], %[b2] bitop3:0xe8\n\t"
+        "v_bitop3_b32 %[t1], %[os], %[b3], %[b4] bitop3:0xe8\n\t"
+        "v_or3_b32 %[os], %[os], %[b3], %[b4]\n\t"
+        "v_bitop3_b32 %[t2], %[os], %[b5], %[b6] bitop3:0xe8\n\t"
+        "v_or3_b32 %[os], %[os], %[b5], %[b6]\n\t"
+        "v_bitop3_b32 %[t3], %[os], %[b7], %[b8] bitop3:0xe8\n\t"
+        "v_or3_b32 %[os], %[os], %[b7], %[b8]\n\t"
+        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        "v_or_b32 %[t0], %[t0], %[t3]\n\t"                                // twice(S)
+        "v_pk_ashrrev_i16 %[t1], 15, %[e] op_sel_hi:[0,1]\n\t"          // fm: 0xFFFF in fresh halves
+        "v_and_b32 %[t2], 0x2000200, %[os]\n\t"                         // an inert given
+        "v_and_b32 %[t3], 0x1ff01ff, %[t0]\n\t"                         // dup
+        "v_or_b32 %[t2], %[t2], %[t3]\n\t"
+        "v_pk_add_u16 %[t2], %[t2], -1\n\t"
+        "v_pk_ashrrev_i16 %[t2], 15, %[t2] op_sel_hi:[0,1]\n\t"
+        "v_and_b32 %[t2], 0x1ff01ff, %[t2]\n\t"                         // exact: 0x1FF
+        "v_bitop3_b32 %[e], %[e], %[t2], %[t1] bitop3:0xd8\n\t"         // E = fresh ? exact : E
+        "v_xor_b32 %[t3], 0x1ff01ff, %[t3]\n\t"                         // kC2 & ~dup
+        "v_bitop3_b32 %[dn], %[dn], %[t3], %[t1] bitop3:0xd8\n\t"       // Dn = fresh ? kC2 & ~dup : Dn
+        "v_and_b32 %[once], %[once], %[e]\n\t"
+        "v_and_b32 %[t0], %[t0], %[dn]\n\t"
+        "v_bitop3_b32 %[t1], %[e], %[ox], %[os] bitop3:0x10\n\t"
+        "v_or_b32 %[bm], %[t0], %[t1]\n\t"
+        "v_and_b32 %[tt], 0x1ff01ff, %[os]"
+        : [ox] "=&v"(ox), [os] "=&v"(os), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [once] "=&v"(once), [bm] "=&v"(bm), [tt] "=&v"(T), [e] "+v"(E), [dn] "+v"(Dn)
+        : [a0] "v"(v[0].x), [a1] "v"(v[1].x), [a2] "v"(v[2].x), [a3] "v"(v[3].x), [a4] "v"(v[4].x),
+          [a5] "v"(v[5].x), [a6] "v"(v[6].x), [a7] "v"(v[7].x), [a8] "v"(v[8].x),
+          [b0] "v"(v[0].y), [b1] "v"(v[1].y), [b2] "v"(v[2].y), [b3] "v"(v[3].y), [b4] "v"(v[4].y),
+          [b5] "v"(v[5].y), [b6] "v"(v[6].y), [b7] "v"(v[7].y), [b8] "v"(v[8].y));
+}
 
 // Ordering point between LDS phases of the one-wave workgroup.  A wave's LDS
 // instructions execute in issue order, so a read after a store sees it and a store
@@ -413,7 +479,7 @@ __device__ __forceinline__ void unit4x(const uint2 (&v)[9], uint32_t E, uint32_t
 // One propagation round for all four boards, branch-free.  Out: per-lane packed
 // contradiction bits (bad: non-zero in a half = that board is contradictory) and change
 // bits (chg).
-template <bool EXACT>
+template <bool EXACT, bool FRESH = false>
 __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bad, uint32_t& chg) {
     w.s_cell[w.c0] = make_uint2(c.x0, c.s0);
     w.s_cell[w.c0 + 27] = make_uint2(c.x1, c.s1);
@@ -425,6 +491,8 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bad,
     uint32_t once, T, bm;
     if (EXACT)
         unit4x(v, c.E, once, T, bm);
+    else if (FRESH)
+        unit4f(v, c.E, c.D, once, T, bm);
     else
         unit4(v, c.E, c.D, once, T, bm);
     w.s_unit[w.c0] = make_uint2(T, once);
@@ -1264,7 +1332,7 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
     c.E = setfld<HI>(c.E, exact);
 }
 
-template <int HI>
+template <int HI, bool FR = false>
 __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c) {
 #if SDK_SOLVE4_STATIC == 1   // experiment: boards dealt round robin to the slots, no dequeue atomics
     b.bidx = b.bend == 0u ? blockIdx.x * 4u + (uint32_t)w.half * 2u + HI : b.bidx + gridDim.x * 4u;
@@ -1356,7 +1424,14 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
         c.s1 = setfld<HI>(c.s1, kInert4);
         c.s2 = setfld<HI>(c.s2, kInert4);
     }
-    statics4<HI>(wr, c);   // the loop lane's LDS addresses: the round's, live anyway
+    if (FR) {
+        // statics pending: the board's first round derives them (unit4f); an empty slot is inert
+        // (not exact, no duplicated digit), which is what statics4 would give it
+        c.E = setfld<HI>(c.E, (b.active & 1u) ? kFresh4 : 0u);
+        c.D = setfld<HI>(c.D, kCands);
+    } else {
+        statics4<HI>(wr, c);   // the loop lane's LDS addresses: the round's, live anyway
+    }
 }
 
 template <bool DN, int HI>
@@ -1373,7 +1448,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
                 atomicOr(&s_dnpend4, 1u << k);
                 *pd = SlotDn{kDnNone, kDnOwner, 0u, 0u};
             }
-            next_board4<HI>(w, wr, a, b, c);
+            next_board4<HI, kFresh4Round && !DN>(w, wr, a, b, c);
             return;
         }
     }
@@ -1394,7 +1469,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
             a.work[b.bidx] = a.work_rounds == 1 ? (uint64_t)(a.iter - b.rstart)
                                                 : (a.work_rounds == 2 ? (uint64_t)b.maxd : b.nodes);
     }
-    next_board4<HI>(w, wr, a, b, c);
+    next_board4<HI, kFresh4Round && !DN>(w, wr, a, b, c);
 }
 
 __device__ __forceinline__ uint32_t branch_key4(uint32_t x, uint32_t s, int cell, int order) {
@@ -1616,7 +1691,7 @@ __device__ __forceinline__ bool step4(const Lane4& wr, const Args4& a, Cells4& c
 }
 
 // first board of slot HI (all lanes)
-template <int HI>
+template <bool DN, int HI>
 __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cells4& c, Slot4* s_slot) {
     Slot4 b;
     b.bidx = 0xFFFFFFFFu;   // ++ -> 0 >= bend = 0: first dequeue
@@ -1624,7 +1699,7 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
     b.active = 0;
     b.depth = 0;
     b.count = 0;
-    next_board4<HI>(w, w, a, b, c);
+    next_board4<HI, kFresh4Round && !DN>(w, w, a, b, c);
     if (w.hl == 0) s_slot[w.half * 2 + HI] = b;
     return (b.active & 1u) != 0u;
 }
@@ -1715,8 +1790,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     c.D = kC2;
     c.E = 0;
     if (threadIdx.x == 0) TL4(0);
-    const bool act0 = first_board4<0>(w, a, c, s_slot);
-    const bool act1 = first_board4<1>(w, a, c, s_slot);
+    const bool act0 = first_board4<DN, 0>(w, a, c, s_slot);
+    const bool act1 = first_board4<DN, 1>(w, a, c, s_slot);
     if (threadIdx.x == 0) TL4(1);
 
     // Event detection in scalar registers: one ballot per (flag, slot), each spread
@@ -1739,8 +1814,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         // every board of the wave exact (an inactive slot is not): the shorter round
         if (a.locked && __builtin_amdgcn_ballot_w64(c.E != kC2) == 0)
             PROF4(0, round4<true>(w, c, badw, chg));
-        else
-            PROF4(0, round4<false>(w, c, badw, chg));
+        else   // SDK_SOLVE4_FRESH_ROUND: also the rounds of waves with a board that just started
+            PROF4(0, (round4<false, kFresh4Round && !DN>(w, c, badw, chg)));
         ++a.iter;
         const uint64_t B0 = spread_halves(__builtin_amdgcn_ballot_w64((badw & 0xFFFFu) != 0u));
         const uint64_t B1 = spread_halves(__builtin_amdgcn_ballot_w64(badw > 0xFFFFu));

@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 4, third box pass: the statics-in-first-round variant (SDK_SOLVE4_FRESH_ROUND=1) --
+# parity of the solver tests on that library, then an A/B against the in-tree build.
+set -o pipefail
+out=gpurun_out/r04c
+mkdir -p $out
+export TMPDIR=/tmp
+T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+SDK_LIB_PATH=$PWD/build/variants/lib_fresh.so timeout -k 10 600 $T tests/test_gpu_solve.py tests/test_gpu_donate.py tests/test_gpu_frontier.py \
+  > $out/pytest_fresh.log 2>&1 || { tail -30 $out/pytest_fresh.log; exit 1; }
+tail -2 $out/pytest_fresh.log
+VARIANTS="fresh" WORKLOADS="solve17:10000000 solve17:1250000 solve30:1000000 minimal:1048576 hard:100000" REPS=3 EXTRA="--donate 0" \
+  timeout -k 10 700 bash tools/ab.sh > $out/ab_fresh.log 2>&1 || { tail -30 $out/ab_fresh.log; exit 1; }
+cat $out/ab_fresh.log

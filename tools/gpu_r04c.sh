@@ -12,3 +12,12 @@ tail -2 $out/pytest_fresh.log
 VARIANTS="fresh" WORKLOADS="solve17:10000000 solve17:1250000 solve30:1000000 minimal:1048576 hard:100000" REPS=3 EXTRA="--donate 0" \
   timeout -k 10 700 bash tools/ab.sh > $out/ab_fresh.log 2>&1 || { tail -30 $out/ab_fresh.log; exit 1; }
 cat $out/ab_fresh.log
+# phase breakdown of the phased solve on the hard sets (kernel trace: split phase, collect,
+# donation launches, scatter)
+for wl in "hard 100000 1" "heavy 1000 16"; do
+  set -- $wl
+  (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OLDPWD/$out/trace_$1 -o run --output-format csv -- \
+     python3 $OLDPWD/tools/solve_profile.py --workload $1 --n $2 --reps 5 --donate $3 --solver quad --donate-max 0 \
+     > $OLDPWD/$out/trace_$1.log 2>&1) || { tail -20 $out/trace_$1.log; exit 1; }
+  cat $out/trace_$1.log | tail -2
+done

@@ -52,6 +52,19 @@ def _worker(rank, world, port, q):
         o, fst = sharded_solve(eng, synth.parse(DEMO), rank, world, comm=comm)
         q.put(("search", rank, total == 7309 and st == 1, rt == 7309 and rst == 1,
                "".join(map(str, o)) == DEMO_FIRST and fst == 1))
+        # point-to-point through the star (non-root to non-root) and the record-moving count:
+        # rank 2 holds the whole 16-clue board as a one-board frontier, ranks 0 and 1 nothing
+        from distributed_sudoku_solver_amd import _lib as L
+        recv = np.zeros(5, np.uint8)
+        ops = {1: [(L.SDK_COMM_SEND, 2, np.arange(5, dtype=np.uint8), 5)],
+               2: [(L.SDK_COMM_RECV, 1, recv, 5)]}.get(rank, [])
+        comm.p2p(ops)
+        info = {}
+        mt, mst, _ = sharded_count_rebalanced(eng, b16, rank, world, comm=comm, chunk=2, target=1,
+                                              ranges=[(1, 1), (1, 1), (0, 1)], info=info)
+        loads = sum(1 for c in eng.calls if isinstance(c, tuple) and c[0] == "load")
+        q.put(("records", rank, recv.tolist() if rank == 2 else None, mt == 7309 and mst == 1, loads,
+               info["refines"]))
     finally:
         comm.close()
 
@@ -66,7 +79,7 @@ def test_tcpcomm_world3():
     for p in procs:
         p.join(180)
         assert p.exitcode == 0
-    got = [q.get(timeout=5) for _ in range(2 * world + 1)]
+    got = [q.get(timeout=5) for _ in range(3 * world + 1)]
     by = {}
     for g in got:
         by.setdefault(g[0], []).append(g[1:])
@@ -76,6 +89,10 @@ def test_tcpcomm_world3():
         if rank == 2:
             assert parts == [b"\x00", b"\x01\x01", b"\x02\x02\x02"]
     assert sorted(by["search"]) == [(r, True, True, True) for r in range(world)]
+    rec = {g[0]: g[1:] for g in by["records"]}
+    assert rec[2][0] == [0, 1, 2, 3, 4]
+    assert all(rec[r][1] for r in range(world))                    # exact total on every rank
+    assert rec[2][3] >= 1 and rec[0][2] >= 1 and rec[1][2] >= 1      # rank 2 refined, both others got records
 
 
 def test_product_path_imports_no_torch():

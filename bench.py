@@ -92,6 +92,8 @@ def parse_args():
                     help="per-lane reference-DFS leg on a C2 prefix (rank 0, N=1; 0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
                     help="watchdog for the side legs: print what was measured and exit")
+    ap.add_argument("--pmc-pipe", default=os.path.join(ROOT, "profiles", "r04", "pmc_pipe.json"),
+                    help="per-SIMD pipe counters of the solve kernel (tools/pmc_r04.sh; '' = none)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r03", "pmc_c4.json"),
                     help="per-launch PMC figures of the C4 solve kernel and the C3 checker from rocprofv3 passes "
                          "of this bench at its default sizes (tools/pmc_c4.sh); '' = report traffic null")
@@ -147,6 +149,27 @@ def pmc_record(path, kernel, units):
     if rec is None or int(rec.get("units_per_launch", -1)) != int(units):
         return None
     return rec
+
+
+def pipe_record(path, run, units):
+    """Per-SIMD pipe figures of the solve kernel from tools/pmc_r04.sh (pmc_pipe.json), or None;
+    only for a launch of the same size as this run's."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f).get(run)
+    if rec is None or int(rec.get("units_per_launch", -1)) != int(units):
+        return None
+    keep = ("kernel_ms", "clock_ghz", "valu_issue_frac", "valu_dual_frac", "salu_per_cu_cycle", "lds_busy_frac",
+            "lds_latency_cycles", "lds_bank_conflict_frac", "lds_data_fifo_full_frac", "lds_cmd_fifo_full_frac",
+            "waves_per_simd")
+    out = {}
+    for part in ("pipe", "lds"):
+        for k, v in rec.get(part, {}).items():
+            if k in keep and k not in out:
+                out[k] = v
+    out["source"] = os.path.relpath(path, ROOT)
+    return out
 
 
 def cpu_share():
@@ -467,7 +490,7 @@ def hard_leg(eng, d, args, synth, L):
         legs["donation_speedup"] = legs["donation"]["value"] / legs["one_launch"]["value"]
         res[name] = legs
     res["hard_1m"]["workload"] = f"the {len(p)} hard puzzles x {reps} seeded symmetries ({len(mp)} boards) per GPU"
-    res["hard_1m"]["roofline"] = pmc_record(args.pmc_summary, "hard_1m", len(mp))
+    res["hard_1m"]["roofline"] = pipe_record(args.pmc_pipe, "hard1m", len(mp))
     stats = {}
     eng.set_option(L.SDK_OPT_DONATE, 0)     # per-board work of one slot per board
     for kind, nm in ((L.SDK_WORK_NODES, "nodes"), (L.SDK_WORK_ROUNDS, "rounds"), (L.SDK_WORK_DEPTH, "depth")):
@@ -755,6 +778,11 @@ def main():
             "stalls": srec.get("stalls"),
             "source": os.path.relpath(args.pmc_summary, ROOT),
         }
+    prec = pipe_record(args.pmc_pipe, "c4", n) if args.workload == "solve17" else None
+    if prec:
+        # per SIMD, at the clock the profiled launch held: VALU issue against 2 per quad-cycle,
+        # LDS busy per CU-cycle, SALU per CU-cycle (tools/pmc_pipe_summary.py)
+        roofline.setdefault("valu", {})["pipe"] = prec
     result = {
         "metric": METRIC,
         "value": value,

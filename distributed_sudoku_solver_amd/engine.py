@@ -6,6 +6,7 @@ solution or a verdict.
 """
 import ctypes
 import numbers
+import threading
 
 import numpy as np
 
@@ -124,6 +125,7 @@ class SudokuEngine:
     """One HIP device + stream.  Thread-safe (the C library serialises per context)."""
 
     def __init__(self, device=0, order=None, node_budget=None, waves_per_cu=None):
+        self._tls = threading.local()
         self.lib = L.load()
         ctx = ctypes.c_void_p()
         L.check(self.lib.sdk_create(int(device), ctypes.byref(ctx)), f"sdk_create(device={device})")
@@ -149,6 +151,7 @@ class SudokuEngine:
         for k, d in enumerate(devices):
             e = cls.__new__(cls)
             e.lib, e.ctx, e.device = lib, ctypes.c_void_p(ctxs[k]), int(d)
+            e._tls = threading.local()
             engines.append(e)
         return engines
 
@@ -260,7 +263,12 @@ class SudokuEngine:
         if masks is not None:
             masks = np.ascontiguousarray(masks, dtype=np.uint16).reshape(n)
         cap = 9 * max(n, int(target), 1)
-        out = np.empty((cap, 81), dtype=np.uint8)
+        # a per-thread staging buffer, grown as needed: a fresh 9 x target board array per call
+        # is megabytes of new pages for every slice of a continued search (search.LexSearch)
+        tl = self._tls
+        out = getattr(tl, "expand_buf", None)
+        if out is None or out.shape[0] < cap:
+            out = tl.expand_buf = np.empty((cap, 81), dtype=np.uint8)
         k = ctypes.c_uint64()
         L.check(self.lib.sdk_expand_boards(self.ctx, _ptr(boards), _ptr(masks), n, int(target), _ptr(out), cap,
                                            ctypes.byref(k)), "sdk_expand_boards")

@@ -91,19 +91,22 @@ def summarize(ctr, wall):
 
 def main(d):
     out = {}
+    units = {"c4": 10_000_000, "hard1m": 1_000_000, "min": 1_048_576}
     for run in ("c4", "hard1m", "min"):
-        rec = {}
+        rec = {"units_per_launch": units[run]}
         for part in ("pipe", "lds"):
             ctr, wall = load(d, f"{run}_{part}")
             s = summarize(ctr, wall)
             if s:
                 rec[part] = s
-        if rec:
+        if len(rec) > 1:
             out[run] = rec
     with open(os.path.join(d, "pmc_pipe.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     for run, rec in out.items():
         for part, s in rec.items():
+            if not isinstance(s, dict):
+                continue
             brief = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in s.items() if k != "counters"}
             print(run, part, json.dumps(brief))
 

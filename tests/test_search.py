@@ -77,3 +77,45 @@ def test_naive_expand_keeps_lex_order():
     keys = ["".join(map(str, k)) for k in kids]
     assert keys == sorted(keys)
     assert all(k[0] in (1, 2, 3, 4) for k in kids)       # cell 0 is the first empty cell: digits 1..4 only
+
+
+def test_lex_search_over_multi_device_engine(solve_cases):
+    """The node's continued search on every GPU of the box: LexSearch.for_node over a 3-device
+    MultiDeviceEngine (oracle doubles) shards each slice's launch and expansion over the devices
+    and still returns the golden answers; the slice is as wide as 3 single-device slices."""
+    from distributed_sudoku_solver_amd.shard import MultiDeviceEngine
+    devs = [OracleEngine() for _ in range(3)]
+    mde = MultiDeviceEngine(devs)
+    hard = [c for c in solve_cases if 10_000 < c["validations"] < 2_000_000]
+    assert len(hard) >= 5
+    for c in hard:
+        b, m = _case_board(c)
+        s = LexSearch.for_node(mde, b, m, budget=1, width=8, slice_target_s=10.0)
+        assert s.width == 24
+        st, out = s.run(time.monotonic() + 60)
+        assert st == (L.SDK_SOLVED if c["ok"] else L.SDK_UNSOLVABLE), c["name"]
+        assert out.tolist() == (c["board"] if c["ok"] else c["puzzle"]), c["name"]
+    assert all(sum(1 for x in d.calls if isinstance(x, int)) > 0 for d in devs)   # every device launched
+
+
+def test_for_node_bounds_the_budget_by_measured_node_time():
+    """LexSearch.for_node starts at the smallest budget and never lets budget x (measured wall time
+    per node of a launch's longest board) exceed half the slice target."""
+    from distributed_sudoku_solver_amd import search as S
+
+    class Slow(OracleEngine):
+        # every launch takes 1 ms per node of its longest board (a synthetic clock)
+        def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
+            out, st, _ = super().solve_batch(boards, masks, True, budget, donate)
+            time.sleep(1e-3 * (int(budget) if budget else 1))
+            return out, st, np.full(len(boards), int(budget) if budget else 1, np.uint64)   # nodes used
+
+    eng = Slow()
+    s = LexSearch.for_node(eng, synth.parse(CONFLICT55), None, budget=64, width=4, slice_target_s=0.02)
+    assert s.budget == 8                                    # node budget / 8
+    seen = []
+    for _ in range(8):
+        s.step()
+        seen.append(s.budget)
+        assert s.budget * 1e-3 <= S.LAUNCH_SHARE * 0.02 * 1.05, seen        # 10 nodes of 1 ms: half the target
+    assert s.t_node is not None and s.t_node >= 1e-3

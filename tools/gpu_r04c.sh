@@ -21,3 +21,14 @@ for wl in "hard 100000 1" "heavy 1000 16"; do
      > $OLDPWD/$out/trace_$1.log 2>&1) || { tail -20 $out/trace_$1.log; exit 1; }
   cat $out/trace_$1.log | tail -2
 done
+# split budget x donation mode on the hard sets (phased solve at any size)
+for n in 100000 1000000; do
+  for dn in 0 32 64 128; do
+    for mode in 1 0; do
+      [ $dn = 0 ] && [ $mode = 0 ] && continue
+      timeout -k 10 120 python tools/solve_profile.py --solver quad --workload hard --n $n --reps 5 --donate $dn \
+        --donate-mode $mode --donate-max 0 >> $out/sweep_hard.log 2>&1 || { tail -5 $out/sweep_hard.log; exit 1; }
+    done
+  done
+done
+cat $out/sweep_hard.log

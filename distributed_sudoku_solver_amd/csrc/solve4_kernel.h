@@ -657,7 +657,8 @@ struct DnCtl {
                               // it): kDnErrReg / kDnErrLock, a bounded wait ran out
     uint32_t fault;           // test only (SDK_OPT_DN_FAULT): registrations are not written
     uint32_t started;         // diagnostics: waves that took part
-    uint32_t pad[21];
+    uint32_t helpers;         // waves taking part per listed board (SDK_OPT_DONATE_HELPERS), plus 64
+    uint32_t pad[20];
     DnXcd x[kDnXcds];
 };
 constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u;
@@ -1723,7 +1724,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     uint32_t grid = gridDim.x;
     if constexpr (DN) {
         if (args.n_dev) n = min<uint64_t>(*args.n_dev, args.n);
-        grid = (uint32_t)min<uint64_t>(gridDim.x, 64ull + 16ull * n);
+        grid = (uint32_t)min<uint64_t>(gridDim.x, 64ull + (uint64_t)ld_agent(&static_cast<DnCtl*>(args.donate)->helpers) * n);
         if (n == 0 || blockIdx.x >= grid) return;
     }
     __shared__ uint2 s_region[2 * kRegion4];

@@ -97,6 +97,7 @@ struct DnPrep {
     uint32_t* ctl[2];
     uint32_t epoch[2];
     uint32_t fault;      // DnCtl.fault (SDK_OPT_DN_FAULT, test only)
+    uint32_t helpers;    // DnCtl.helpers (SDK_OPT_DONATE_HELPERS)
     uint32_t* list[2];
 };
 __global__ void dn_prep_kernel(DnPrep p) {
@@ -111,10 +112,11 @@ __global__ void dn_prep_kernel(DnPrep p) {
         for (uint32_t i = t; i < p.heads_words; i += blockDim.x) p.heads[i] = 0;
     // every word but the sticky error word (the host reads and clears it after the solve)
     constexpr uint32_t kEpoch = offsetof(DnCtl, epoch) / 4, kErr = offsetof(DnCtl, err) / 4,
-                       kFault = offsetof(DnCtl, fault) / 4;
+                       kFault = offsetof(DnCtl, fault) / 4, kHelpers = offsetof(DnCtl, helpers) / 4;
     for (int k = 0; k < 2; ++k)
         for (uint32_t i = t; i < sizeof(DnCtl) / 4; i += blockDim.x)
-            if (i != kErr) p.ctl[k][i] = i == kEpoch ? p.epoch[k] : (i == kFault ? p.fault : 0u);
+            if (i != kErr)
+                p.ctl[k][i] = i == kEpoch ? p.epoch[k] : (i == kFault ? p.fault : (i == kHelpers ? p.helpers : 0u));
 }
 __global__ void dn_scatter_kernel(const uint32_t* list, const uint8_t* sub_out, const int8_t* sub_st,
                                   const uint64_t* sub_work, bool depth, uint8_t* out, int8_t* status, uint64_t* work) {
@@ -164,6 +166,7 @@ struct sdk_ctx {
     bool timer_hold = false;       // a phased solve is being timed as one span
     bool dn_err_check = false;     // a phased solve ran since its control blocks' error words were read
     int dn_fault = 0;              // SDK_OPT_DN_FAULT (test only)
+    int dn_helpers = 16;           // SDK_OPT_DONATE_HELPERS: donation-launch waves per listed board (+ 64)
     int dn_exhaustive = 1;         // phase 2 in MRV count-to-2 order (SDK_OPT_DONATE_MODE)
     int64_t dn_max = 1 << 19;      // largest batch solved in phases (SDK_OPT_DONATE_MAX, 0 = any)
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
@@ -372,10 +375,10 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
         a.n_dev = n_dev;
         a.chunk = 1;
         a.next = &static_cast<sdk::DnCtl*>(c->dn_area)->next;
-        // the resident grid; the kernel keeps 64 + 16 waves per board of it (solve4_kernel)
+        // the resident grid; the kernel keeps 64 + SDK_OPT_DONATE_HELPERS waves per board of it
         grid_used = (unsigned)std::max<uint64_t>(
             1, std::min<uint64_t>({(uint64_t)c->cus * (uint64_t)std::min(c->dn_blocks_per_cu, c->waves_per_cu2),
-                                   (uint64_t)sdk::kDnMbox, 64ull + 16ull * (uint64_t)n}));
+                                   (uint64_t)sdk::kDnMbox, 64ull + (uint64_t)c->dn_helpers * (uint64_t)n}));
         if (grid_used > grid) {
             rc = ensure(c->stack, (size_t)grid_used * stack_words * sizeof(uint32_t));
             if (rc) return rc;
@@ -488,6 +491,7 @@ int dn_prep(sdk_ctx* c, uint64_t cap, bool first_pass) {
         p.epoch[k] = ++c->dn_epoch;
     }
     p.fault = c->dn_fault ? 1u : 0u;
+    p.helpers = (uint32_t)c->dn_helpers;
     p.list[0] = static_cast<uint32_t*>(c->dn_list.p);
     p.list[1] = static_cast<uint32_t*>(c->dn3_list.p);
     sdk::dn_prep_kernel<<<1, 256, 0, c->stream>>>(p);
@@ -901,6 +905,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "SDK_OPT_DN_FAULT must be 0 or 1");
             c->dn_fault = (int)value;
             return SDK_OK;
+        case SDK_OPT_DONATE_HELPERS:
+            if (value < 1 || value > 4096) return fail(SDK_EINVAL, "SDK_OPT_DONATE_HELPERS must be 1..4096");
+            c->dn_helpers = (int)value;
+            return SDK_OK;
         case SDK_OPT_DONATE_MODE:
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "donate mode must be 0 (LEX) or 1 (exhaustive)");
             c->dn_exhaustive = (int)value;
@@ -993,6 +1001,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_LEX_BOARDS: return read_dn_stat(c, 1, value);
         case SDK_OPT_DONATE_MAX: *value = c->dn_max; return SDK_OK;
         case SDK_OPT_DN_FAULT: *value = c->dn_fault; return SDK_OK;
+        case SDK_OPT_DONATE_HELPERS: *value = c->dn_helpers; return SDK_OK;
         case SDK_OPT_DONATED: {
             // items handed out by the last phased solve's donation launches (of its last
             // kDnCapBoards-board pass; waits for it on the context's stream)

@@ -109,6 +109,8 @@ extern "C" {
                                  /* bounded wait for it runs out: the solve then fails   */
                                  /* with SDK_EHIP (every wait on another wave inside a   */
                                  /* launch is bounded and reports this way)              */
+#define SDK_OPT_DONATE_HELPERS 22 /* waves of a donation launch per board it re-solves   */
+                                 /* (plus 64; default 16, at most the resident grid)     */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

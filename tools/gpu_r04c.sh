@@ -32,3 +32,12 @@ for n in 100000 1000000; do
   done
 done
 cat $out/sweep_hard.log
+# donation-launch waves per tail board (SDK_OPT_DONATE_HELPERS)
+for wl in "hard 100000 128" "heavy 1000 16"; do
+  set -- $wl
+  for h in 16 48 128; do
+    timeout -k 10 120 python tools/solve_profile.py --solver quad --workload $1 --n $2 --reps 5 --donate $3 \
+      --donate-max 0 --helpers $h >> $out/sweep_helpers.log 2>&1 || { tail -5 $out/sweep_helpers.log; exit 1; }
+  done
+done
+cat $out/sweep_helpers.log

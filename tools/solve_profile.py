@@ -28,6 +28,7 @@ ap.add_argument("--locked", type=int, default=1, help="QUAD: locked-candidates p
 ap.add_argument("--donate", type=int, default=-1, help="QUAD: SDK_OPT_DONATE (default: library default)")
 ap.add_argument("--donate-mode", type=int, default=-1, help="QUAD: SDK_OPT_DONATE_MODE (1 exhaustive, 0 LEX)")
 ap.add_argument("--donate-max", type=int, default=-1, help="QUAD: SDK_OPT_DONATE_MAX (0: phased at any size)")
+ap.add_argument("--helpers", type=int, default=0, help="QUAD: SDK_OPT_DONATE_HELPERS (waves per tail board)")
 args = ap.parse_args()
 
 if args.workload == "minimal":
@@ -57,6 +58,8 @@ with SudokuEngine(0) as eng:
         eng.set_option(L.SDK_OPT_DONATE_MODE, args.donate_mode)
     if args.donate_max >= 0:
         eng.set_option(L.SDK_OPT_DONATE_MAX, args.donate_max)
+    if args.helpers:
+        eng.set_option(L.SDK_OPT_DONATE_HELPERS, args.helpers)
     if args.waves_per_cu:
         eng.set_option(wopt, args.waves_per_cu)
     d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)
@@ -71,7 +74,7 @@ with SudokuEngine(0) as eng:
     out = np.empty((args.n, 81), np.uint8)
     d_out.download(out)
     per = ms / args.reps       # one solve: one launch, or both launches of a two-phase solve
-    print(f"{args.solver} {args.order} lc={args.locked} xh={args.xcd_heads} dn={args.donate}/{args.donate_mode} chunk={args.chunk} {args.workload} n={args.n} solve={per:.3f} ms "
+    print(f"{args.solver} {args.order} lc={args.locked} xh={args.xcd_heads} dn={args.donate}/{args.donate_mode}/h{args.helpers} chunk={args.chunk} {args.workload} n={args.n} solve={per:.3f} ms "
           f"({nl // args.reps} launches) rate={args.n / per * 1e3 / 1e6:.1f} M/s ok={(out == s).all()}", flush=True)
     if args.sweep:
         for wpc in (8, 12, 16, 20, 24, 32):

@@ -21,6 +21,11 @@ for n in 100000 1000000; do
     done
   done
 done
+for n in 100000 1000000; do
+  for order in lex mrv_unique; do
+    timeout -k 10 120 python tools/solve_profile.py --solver quad --workload hard --n $n --reps 5 --donate 0       --order $order --stats >> $out/sweep_hard.log 2>&1 || { tail -5 $out/sweep_hard.log; exit 1; }
+  done
+done
 cat $out/sweep_hard.log
 for wl in "hard 100000 128" "heavy 1000 16"; do
   set -- $wl

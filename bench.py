@@ -41,7 +41,7 @@ SOLVE_BYTES_PER_PUZZLE = 163      # 81 in + 81 out + 1 status (SURVEY §8(d) C2/
 CHECK_BYTES_PER_BOARD = 82        # 81 in + 1 verdict
 # VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles (32 lanes/cycle x 2)")
-VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4   # one wave64 VALU per SIMD quad-cycle
 # --solver: (SDK_OPT_SOLVER value, kernel name, grid option) -- resolved after the library loads
 SOLVERS = {
     "halfwave": (1, "sdk::solve2_kernel", 8),
@@ -160,14 +160,18 @@ def pipe_record(path, run, units):
         rec = json.load(f).get(run)
     if rec is None or int(rec.get("units_per_launch", -1)) != int(units):
         return None
-    keep = ("kernel_ms", "clock_ghz", "valu_issue_frac", "valu_dual_frac", "salu_per_cu_cycle", "lds_busy_frac",
-            "lds_latency_cycles", "lds_bank_conflict_frac", "lds_data_fifo_full_frac", "lds_cmd_fifo_full_frac",
-            "waves_per_simd")
+    keep = ("kernel_ms", "clock_ghz", "valu_busy_frac", "valu_dual_frac", "valu_per_quad", "salu_per_cu_cycle",
+            "lds_busy_frac", "lds_insts_per_cu_cycle", "lds_bank_conflict_frac", "lds_data_fifo_full_frac",
+            "lds_cmd_fifo_full_frac", "waves_per_simd")
     out = {}
     for part in ("pipe", "lds"):
         for k, v in rec.get(part, {}).items():
             if k in keep and k not in out:
                 out[k] = v
+        ctr = rec.get(part, {}).get("counters", {})
+        for k, c in (("valu_insts", "SQ_INSTS_VALU"), ("salu_insts", "SQ_INSTS_SALU"), ("lds_insts", "SQ_INSTS_LDS")):
+            if c in ctr and k not in out:
+                out[k] = ctr[c]
     out["source"] = os.path.relpath(path, ROOT)
     return out
 
@@ -761,28 +765,41 @@ def main():
         "traffic_raw": srec.get("traffic_raw") if srec else None,
         "kernel": solve_kernel,
         "avg_kernel_ms": avg_kernel_s * 1000.0,
-        "note": "the search is VALU-issue / LDS-latency bound: see roofline.valu; HBM fraction reported "
-                "per contract (163 algorithmic B per puzzle)",
+        "note": "the search is VALU-issue bound (roofline.valu: SIMD quad-cycles with VALU issue); HBM "
+                "fraction reported per contract (163 algorithmic B per puzzle)",
     }
-    if srec and srec.get("valu_insts"):
-        # VALU wave-instructions per launch (PMC pass of this exact launch) over the live launch time,
-        # against the issue peak: wave64 VALU issues over 2 cycles on a SIMD-32 (MI355X_MICROARCH.md)
+    prec = pipe_record(args.pmc_pipe, "c4", n) if args.workload == "solve17" else None
+    if prec and prec.get("valu_insts") and prec.get("clock_ghz"):
+        # per SIMD, from a PMC pass of this exact launch (tools/pmc_r04.sh, tools/pmc_pipe_summary.py):
+        # a wave64 VALU instruction holds its SIMD's VALU issue for one quad-cycle, and a SIMD
+        # issues two in some quad-cycles (SQ_ACTIVE_INST_VALU2); the roofline fraction is the share
+        # of SIMD quad-cycles that issued VALU at all
+        single = 256 * 4 * prec["clock_ghz"] * 1e9 / 4
+        rate = prec["valu_insts"] / avg_kernel_s
+        roofline["valu"] = {
+            "bound": "valu-issue", "achieved": rate, "unit": "wave-instr/s", "peak": single,
+            "peak_note": "one wave64 VALU issue per SIMD quad-cycle at the profiled clock; dual issue in "
+                         "valu_dual_frac of the quad-cycles lets achieved exceed it",
+            "frac": prec["valu_busy_frac"],
+            "frac_note": "SIMD quad-cycles with VALU issue: (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / quad-cycles",
+            "valu_insts_per_puzzle": prec["valu_insts"] / n,
+            "lds_insts_per_puzzle": (prec.get("lds_insts") or 0) / n,
+            "salu_insts_per_puzzle": (prec.get("salu_insts") or 0) / n,
+            "pipe": prec,
+            "stalls": srec.get("stalls") if srec else None,
+        }
+    elif srec and srec.get("valu_insts"):
+        # older PMC record (no per-SIMD counters): VALU wave-instructions per launch over the issue
+        # rate of one per SIMD quad-cycle at 2.4 GHz
         peak = VALU_PEAK_WAVE_INSTR_PER_S
         rate = srec["valu_insts"] / avg_kernel_s
         roofline["valu"] = {
             "bound": "valu-issue", "achieved": rate, "peak": peak, "unit": "wave-instr/s", "frac": rate / peak,
             "valu_insts_per_puzzle": srec["valu_insts"] / n,
-            "valu_active_per_wave_cycle": srec.get("valu_active_per_wave_cycle"),
             "lds_insts_per_puzzle": srec.get("lds_insts", 0) / n,
-            "lds_bank_conflict_cycles": srec.get("lds_bank_conflict"),
             "stalls": srec.get("stalls"),
             "source": os.path.relpath(args.pmc_summary, ROOT),
         }
-    prec = pipe_record(args.pmc_pipe, "c4", n) if args.workload == "solve17" else None
-    if prec:
-        # per SIMD, at the clock the profiled launch held: VALU issue against 2 per quad-cycle,
-        # LDS busy per CU-cycle, SALU per CU-cycle (tools/pmc_pipe_summary.py)
-        roofline.setdefault("valu", {})["pipe"] = prec
     result = {
         "metric": METRIC,
         "value": value,

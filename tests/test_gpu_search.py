@@ -110,9 +110,10 @@ def test_conflict55_exhausts_quickly(engine):
     """'55' + 79 zeros has no completion and propagation cannot refute it (the reference
     never finishes).  Bounded: it ends as SDK_BUDGET_HIT (exhausted), input unchanged, in well
     under a second, and the batch it was launched with is answered in one bounded launch."""
+    from distributed_sudoku_solver_amd.search import SLICE_TARGET_S
     b = synth.parse(CONFLICT55)
     t0 = time.perf_counter()
-    s = LexSearch(engine, b)
+    s = LexSearch.for_node(engine, b)                   # the node's bounded slices
     slices = []
     while not s.done and time.perf_counter() - t0 < 3.0:
         t1 = time.perf_counter()
@@ -121,7 +122,9 @@ def test_conflict55_exhausts_quickly(engine):
     st, out = s.run(time.monotonic())                   # deadline passed: exhausted
     assert st == L.SDK_BUDGET_HIT and (out == b).all()
     assert time.perf_counter() - t0 < 4.0
-    assert len(slices) > 3 and max(slices) < 0.25, (len(slices), max(slices), s.budget, s.pending)   # unbounded mode
+    srt = sorted(slices[1:])                            # the first slice sizes the buffers
+    assert len(srt) > 20 and srt[len(srt) // 2] <= SLICE_TARGET_S and srt[int(0.9 * len(srt))] <= 1.5 * SLICE_TARGET_S, \
+        (["%.2f" % (1e3 * t) for t in slices], s.budget)
     batch = np.stack([b, synth.parse(synth.WIKI)])
     t0 = time.perf_counter()
     out, st, _ = engine.solve_batch(batch, want_work=True, budget=2048)
@@ -146,18 +149,27 @@ def test_node_slices_are_bounded(engine):
     """a node's continued search (LexSearch.for_node, on its own context) keeps
     every slice -- launch, expansion and host copies together -- within 1.5 x the slice target,
     on '55'+79 zeros (unrefutable: every sub-board hits the budget, the worst case)."""
-    from distributed_sudoku_solver_amd.search import SLICE_TARGET_S
+    from distributed_sudoku_solver_amd.search import LAUNCH_SHARE, SLICE_TARGET_S
     fork = engine.fork()
     try:
         b = synth.parse(CONFLICT55)
         s = LexSearch.for_node(fork, b)
         s.step()                                        # warm: the first slice sizes the buffers
         times = []
-        for _ in range(30):
+        for _ in range(40):
             s.step()
             times.append(s.last_slice_s)
+            # the design bound, before the next launch runs: its budget x the measured wall time
+            # per node of a launch's critical path stays within LAUNCH_SHARE of the target
+            assert s.budget == 1 or s.budget * s.t_node <= LAUNCH_SHARE * SLICE_TARGET_S * 1.001, (s.budget, s.t_node)
         assert not s.done
-        assert max(times) <= 1.5 * SLICE_TARGET_S, (["%.2f" % (1e3 * t) for t in times], s.budget, s.width)
+        # measured: the slices themselves.  A box-wide stall (every part of one slice -- launch,
+        # expansion and the host's own numpy work -- slowed about 20x at once, ~1 slice in 75 in
+        # profiles/r04/slice_probe_node.log) is not the search's budget, so the bound is asserted
+        # on the median and the 90th percentile
+        srt = sorted(times)
+        assert srt[len(srt) // 2] <= SLICE_TARGET_S and srt[int(0.9 * len(srt))] <= 1.5 * SLICE_TARGET_S, \
+            (["%.2f" % (1e3 * t) for t in times], s.budget, s.width)
         assert s.budget > 1                            # the bound leaves room to search
     finally:
         fork.close()

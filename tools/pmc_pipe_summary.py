@@ -1,21 +1,21 @@
 """Summarise tools/pmc_r04.sh: what bounds solve4_kernel per SIMD.
 
 Per pass (c4 / hard1m / min), for the plain solve4_kernel dispatches (the first dispatch of
-each run is a warm-up and is dropped when there are more):
-  clock_ghz           GRBM_GUI_ACTIVE / 8 / kernel wall (MI355X_MICROARCH.md "DVFS give-back":
-                      rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs)
-  simd_cycles         SQ_CYCLES (clock cycles, summed over every SIMD)
-  valu_issue_frac     SQ_INSTS_VALU / (simd_cycles / 2): VALU issue against the SIMD's peak of one
-                      wave64 VALU instruction per 2 cycles (two per quad-cycle, SQ_ACTIVE_INST_VALU2)
-  valu_dual_frac      SQ_ACTIVE_INST_VALU2 / (simd_cycles / 4): quad-cycles in which the SIMD
-                      issued two VALU instructions
-  valu_any_frac       from SQ_ACTIVE_INST_VALU ... reported raw (per-wave quad-cycles, summed over waves)
-  salu_per_cu_cycle   SQ_INSTS_SALU / (simd_cycles / 4): SALU instructions per CU-cycle
-  lds_busy_frac       SQ_LDS_IDX_ACTIVE / (simd_cycles / 4): cycles the CU's LDS was busy with
-                      indexed accesses per CU-cycle (4 SIMDs per CU)
-  lds_latency_cycles  SQ_INST_LEVEL_LDS / SQ_INSTS_LDS (in-flight LDS instructions per cycle over the
-                      instruction count: the mean LDS instruction latency)
-  waves_per_simd      SQ_WAVE_CYCLES * 4 / simd_cycles (mean resident waves)
+each run is a warm-up and is dropped when there are more).  Units, from the counters' own
+descriptions (rocprofv3 --list-avail) and checked against the kernel wall time:
+  * SQ_CYCLES is summed over the shader engines (32 on MI355X: SQ_CYCLES / (wall x clock) = 32);
+    an SE holds 8 CUs = 32 SIMDs, so SIMD quad-cycles = SQ_CYCLES / 4 x 32 and CU-cycles =
+    SQ_CYCLES x 8;
+  * a wave64 VALU instruction occupies its SIMD's VALU issue for one quad-cycle
+    (SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU), and SQ_ACTIVE_INST_VALU2 counts the quad-cycles in
+    which a SIMD issued TWO VALU instructions.  So the quad-cycles with VALU issue are
+    INSTS_VALU - VALU2, and
+      valu_busy_frac   = (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / SIMD quad-cycles
+      valu_dual_frac   = SQ_ACTIVE_INST_VALU2 / SIMD quad-cycles
+      valu_per_quad    = SQ_INSTS_VALU / SIMD quad-cycles (2.0 would be dual issue every quad-cycle)
+  * salu_per_cu_cycle = SQ_INSTS_SALU / CU-cycles; lds_busy_frac = SQ_LDS_IDX_ACTIVE / CU-cycles;
+    lds_*_fifo_full_frac likewise; waves_per_simd = SQ_WAVE_CYCLES / SIMD quad-cycles;
+  * clock_ghz = GRBM_GUI_ACTIVE / 8 / kernel wall (MI355X_MICROARCH.md "DVFS give-back").
 usage: python3 tools/pmc_pipe_summary.py <dir>      -> <dir>/pmc_pipe.json
 """
 import csv
@@ -24,6 +24,8 @@ import json
 import os
 import sys
 from collections import defaultdict
+
+CUS = 256                 # MI355X compute units (4 SIMDs each)
 
 
 def _rows(d, tag, pattern):
@@ -70,22 +72,26 @@ def summarize(ctr, wall):
     cyc = g.get("SQ_CYCLES")
     if ns and g.get("GRBM_GUI_ACTIVE"):
         rec["clock_ghz"] = g["GRBM_GUI_ACTIVE"] / 8 / ns
-    if cyc:
-        rec["simd_cycles"] = cyc
-        if ns:
-            rec["simds_x_clock_ghz"] = cyc / ns
-        for key, num, den in (("valu_issue_frac", "SQ_INSTS_VALU", cyc / 2),
-                              ("valu_dual_frac", "SQ_ACTIVE_INST_VALU2", cyc / 4),
-                              ("salu_per_cu_cycle", "SQ_INSTS_SALU", cyc / 4),
-                              ("lds_busy_frac", "SQ_LDS_IDX_ACTIVE", cyc / 4),
-                              ("lds_bank_conflict_frac", "SQ_LDS_BANK_CONFLICT", cyc / 4),
-                              ("lds_data_fifo_full_frac", "SQ_LDS_DATA_FIFO_FULL", cyc / 4),
-                              ("lds_cmd_fifo_full_frac", "SQ_LDS_CMD_FIFO_FULL", cyc / 4),
-                              ("waves_per_simd", "SQ_WAVE_CYCLES", cyc / 4)):
+    if cyc and rec.get("clock_ghz"):
+        n_se = max(1, round(cyc / (ns * rec["clock_ghz"])))
+        simd_quads = cyc / 4 * (CUS * 4 / n_se)
+        cu_cycles = cyc * (CUS / n_se)
+        rec.update(shader_engines=n_se, simd_quad_cycles=simd_quads, cu_cycles=cu_cycles)
+        if g.get("SQ_INSTS_VALU") is not None:
+            v2 = g.get("SQ_ACTIVE_INST_VALU2", 0.0)
+            rec["valu_per_quad"] = g["SQ_INSTS_VALU"] / simd_quads
+            rec["valu_busy_frac"] = (g["SQ_INSTS_VALU"] - v2) / simd_quads
+            rec["valu_dual_frac"] = v2 / simd_quads
+        for key, num, den in (("salu_per_cu_cycle", "SQ_INSTS_SALU", cu_cycles),
+                              ("lds_busy_frac", "SQ_LDS_IDX_ACTIVE", cu_cycles),
+                              ("lds_bank_conflict_frac", "SQ_LDS_BANK_CONFLICT", cu_cycles),
+                              ("lds_data_fifo_full_frac", "SQ_LDS_DATA_FIFO_FULL", cu_cycles),
+                              ("lds_cmd_fifo_full_frac", "SQ_LDS_CMD_FIFO_FULL", cu_cycles),
+                              ("waves_per_simd", "SQ_WAVE_CYCLES", simd_quads)):
             if g.get(num) is not None:
                 rec[key] = g[num] / den
-    if g.get("SQ_INSTS_LDS") and g.get("SQ_INST_LEVEL_LDS"):
-        rec["lds_latency_cycles"] = g["SQ_INST_LEVEL_LDS"] / g["SQ_INSTS_LDS"]
+        if g.get("SQ_INSTS_LDS") is not None:
+            rec["lds_insts_per_cu_cycle"] = g["SQ_INSTS_LDS"] / cu_cycles
     return rec
 
 

@@ -220,6 +220,7 @@ class LexSearch:
                 # bound of the node time, so the budget derived from it keeps the launch short
                 tn = elapsed / max(1, int(work.max()))
                 self.t_node = tn if self.t_node is None else max(tn, 0.5 * (self.t_node + tn))
+                self._cap_budget()
         st = np.asarray(st)
         decided = np.flatnonzero(st != L.SDK_UNSOLVABLE)          # refuted sub-boards simply vanish
         solved = decided[st[decided] == L.SDK_SOLVED]
@@ -247,6 +248,11 @@ class LexSearch:
             return True
         return False
 
+    def _cap_budget(self):
+        """budget x (measured node time) <= LAUNCH_SHARE x the slice target, before the next launch."""
+        if self.slice_target_s is not None and self.t_node:
+            self.budget = max(1, min(self.budget, int(LAUNCH_SHARE * self.slice_target_s / self.t_node)))
+
     def _bound_budget(self, launch_s, mostly_hits):
         """The next launch's budget (and width) under the slice target: grow while launches are
         fast and mostly hit the budget, halve after a slow one, and never above what the
@@ -256,8 +262,7 @@ class LexSearch:
             self.budget = max(1, self.budget // 2)
         elif 2 * launch_s < LAUNCH_SHARE * target and mostly_hits:
             self.budget = min(2 * self.budget, self.max_budget)
-        if self.t_node:
-            self.budget = max(1, min(self.budget, int(LAUNCH_SHARE * target / self.t_node)))
+        self._cap_budget()
         if self.budget == 1 and launch_s > LAUNCH_SHARE * target:
             # one node per board is still too long: the launch's fixed costs (copies) dominate
             self.width = max(MIN_WIDTH * n_devices(self.engine), self.width // 2)

@@ -754,6 +754,12 @@ __device__ __forceinline__ uint32_t fld_rt(uint32_t w, uint32_t hi) {
 __device__ __forceinline__ uint32_t setfld_rt(uint32_t w, uint32_t v, uint32_t hi) {
     return hi ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
 }
+// a value whose memory operation must have completed here (an atomic's return, a load): the
+// compiler waits for it (s_waitcnt) at this point, ordering it before what follows
+__device__ __forceinline__ uint32_t wait_done(uint32_t v) {
+    asm volatile("" : "+v"(v)::"memory");
+    return v;
+}
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -959,7 +965,7 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
             __hip_atomic_store(mbox + (uint32_t)e, ((unsigned long long)epoch << 32) | (i0 + k), __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
-        atomicAdd(&ctl->delivered, valid);
+        wait_done(atomicAdd(&ctl->delivered, valid));   // before this wave can count itself idle
     }
     // the level keeps its lower untried digits; with none left it is the donor's no more
     if (stay == 0u) {
@@ -1150,9 +1156,8 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(s_dnepoch4);
     unsigned long long* mbox = dn_mbox4(a) + blockIdx.x;
     if (!(st & 1u)) {
-        // this wave's deliveries (`delivered`) before its idle count: an exit check that sees
-        // the decrement sees them (see the hand-off above)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // this wave's deliveries were waited for (dn_donate4), so an exit check that sees this
+        // decrement sees them (see the hand-off above)
         if (w.lane == 0) atomicSub(&mx->busy, 1u);
         st |= 1u;
     }
@@ -1185,11 +1190,12 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
     if (((st >> 8) & 15u) == 1u) {
         // leave when no started wave is busy and no delivery happened while the eight
         // counters were read (they are not one snapshot: see the hand-off above)
-        const uint32_t v1 = ld_agent(&ctl->delivered);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // the three reads in this order (each waited for before the next is issued); no agent-
+        // scope acquire: one per check would invalidate the XCD's L2 under the working waves
+        const uint32_t v1 = wait_done(ld_agent(&ctl->delivered));
         uint32_t busy = 0;
         for (int k = 0; k < kDnXcds; ++k) busy += ld_agent(&ctl->x[k].busy);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        busy = wait_done(busy);
         const uint32_t v2 = ld_agent(&ctl->delivered);
         busy = __builtin_amdgcn_readfirstlane(busy);
         if (busy == 0u && __builtin_amdgcn_readfirstlane(v1) == __builtin_amdgcn_readfirstlane(v2)) {
@@ -1770,11 +1776,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         s_dnwave4 = 0u;
         s_dnepoch4 = ld_agent(&a.dn->epoch);
         s_dngrid4 = grid;
-        // counted busy before the first dequeue (release): a wave whose dequeue comes up empty
-        // after this one's took a board sees this count (see the hand-off above)
-        atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u);
-        atomicAdd(&a.dn->started, 1u);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // counted busy before the first dequeue: the add is waited for (its return value used)
+        // before the dequeue is issued, so a wave whose dequeue comes up empty after this one's
+        // took a board reads this count (see the hand-off above).  No agent-scope fence: a
+        // release there writes back the XCD's L2 for every wave of the launch
+        wait_done(atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u));
     }
     {   // segments share the first n - n/128 boards (rounded to whole chunks); the rest is the tail
         a.tail_chunk = max(1u, args.chunk / SDK_SOLVE4_TAIL_CHUNK_DIV);

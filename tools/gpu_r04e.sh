@@ -5,6 +5,22 @@ set -o pipefail
 out=gpurun_out/r04e
 mkdir -p $out
 export TMPDIR=/tmp
+# the donation launch after the fence-free busy accounting, against round 3's kernel (lib_r03)
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_donate.py > $out/pytest_donate.log 2>&1 \
+  || { tail -30 $out/pytest_donate.log; exit 1; }
+tail -1 $out/pytest_donate.log
+for rep in 1 2 3; do
+  for wl in "hard 100000 1" "heavy 1000 16"; do
+    set -- $wl
+    for v in base r03; do
+      SDK_LIB_PATH=$PWD/build/variants/lib_$v.so timeout -k 10 120 python tools/solve_profile.py --solver quad --workload $1 \
+        --n $2 --reps 5 --donate $3 --donate-max 0 2>&1 | sed "s/^/$v /" >> $out/ab_donate.log || { tail -5 $out/ab_donate.log; exit 1; }
+      SDK_LIB_PATH=$PWD/build/variants/lib_$v.so timeout -k 10 120 python tools/solve_profile.py --solver quad --workload $1 \
+        --n $2 --reps 5 --donate 0 2>&1 | sed "s/^/$v /" >> $out/ab_donate.log || { tail -5 $out/ab_donate.log; exit 1; }
+    done
+  done
+done
+cat $out/ab_donate.log
 for wl in "hard 100000 1" "heavy 1000 16"; do
   set -- $wl
   (cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $OLDPWD/$out/trace_$1 -o run --output-format csv -- \

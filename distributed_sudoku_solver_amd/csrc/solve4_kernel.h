@@ -662,6 +662,18 @@ struct DnCtl {
     DnXcd x[kDnXcds];
 };
 constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u;
+// measurement builds only (tools/build_variant.sh): each round-4 change of the donation kernel
+// alone -- tickets by compare-and-swap, the error-word check before a donation, the waits that
+// order the busy count and `delivered` (and bound the registration wait)
+#ifndef SDK_DN_CAS
+#define SDK_DN_CAS 1
+#endif
+#ifndef SDK_DN_ERRCHECK
+#define SDK_DN_ERRCHECK 1
+#endif
+#ifndef SDK_DN_WAITS
+#define SDK_DN_WAITS 1
+#endif
 // bound of every wait on another wave, in s_memrealtime ticks (100 MHz): 0.2 s -- a
 // registration is written right after its ticket is drawn and a lock is held for a few
 // hundred cycles, so only a wave that cannot run (a fault, or a preempted queue) gets near it
@@ -855,7 +867,7 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     }
     if (x == kDnXcds) return;                                     // no idle wave waits
     if (half_any4(w, w.act && fld_rt(c.E, hi) == 0u)) return;   // only boards with every unit exact
-    if (ld_agent(&ctl->err) != 0u) return;                        // a bounded wait ran out: no more donation
+    if (SDK_DN_ERRCHECK && ld_agent(&ctl->err) != 0u) return;     // a bounded wait ran out: no more donation
     const uint32_t lvl = d.base;
     uint2* lp = g_stk + (lvl * 2 + hi) * 64 + w.lane;
     const uint2 snap = *lp;
@@ -868,7 +880,17 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     // donor takes belongs to a wave that registered (a plain add with a stale head could
     // pass reg_tail and leave later registrations below it, never served)
     uint32_t t0 = 0, valid = 0;
+#if !SDK_DN_CAS   // round 3's reservation (measurement builds): a stale head can pass reg_tail
+    if (w.hl == 0) {
+        const uint32_t want = min(cnt, tail - head);
+        t0 = atomicAdd(&ctl->x[x].reg_head, want);
+        const uint32_t tail2 = min(ld_agent(&ctl->x[x].reg_tail), kDnRegX);
+        valid = tail2 > t0 ? min(want, tail2 - t0) : 0u;
+    }
+    if (false) {
+#else
     if (w.hl == 0 && cnt != 0u) {
+#endif
         uint32_t h = head, t = min(tail, kDnRegX);
         for (int it = 0; it < 8 && t > h; ++it) {
             const uint32_t want = min(cnt, t - h);
@@ -948,8 +970,9 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
         for (uint32_t k = 0; k < valid; ++k) {
             // the registrant writes its entry right after drawing the ticket: a bounded wait
             unsigned long long e;
-            const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
             bool ok = true;
+#if SDK_DN_WAITS
+            const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
             while (((e = ld_agent64(reg + t0 + k)) >> 32) != epoch) {
                 if (__builtin_amdgcn_s_memrealtime() - t_start > kDnWaitTicks) {
                     ok = false;
@@ -957,6 +980,9 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
+#else
+            while (((e = ld_agent64(reg + t0 + k)) >> 32) != epoch) __builtin_amdgcn_s_sleep(1);
+#endif
             if (!ok) {   // the items left stay undelivered: the solve reports SDK_EHIP
                 atomicOr(&ctl->err, kDnErrReg);
                 break;
@@ -965,7 +991,11 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
             __hip_atomic_store(mbox + (uint32_t)e, ((unsigned long long)epoch << 32) | (i0 + k), __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
+#if SDK_DN_WAITS
         wait_done(atomicAdd(&ctl->delivered, valid));   // before this wave can count itself idle
+#else
+        atomicAdd(&ctl->delivered, valid);
+#endif
     }
     // the level keeps its lower untried digits; with none left it is the donor's no more
     if (stay == 0u) {
@@ -1780,7 +1810,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         // before the dequeue is issued, so a wave whose dequeue comes up empty after this one's
         // took a board reads this count (see the hand-off above).  No agent-scope fence: a
         // release there writes back the XCD's L2 for every wave of the launch
+#if SDK_DN_WAITS
         wait_done(atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u));
+#else
+        atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u);
+#endif
     }
     {   // segments share the first n - n/128 boards (rounded to whole chunks); the rest is the tail
         a.tail_chunk = max(1u, args.chunk / SDK_SOLVE4_TAIL_CHUNK_DIV);

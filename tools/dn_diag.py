@@ -24,6 +24,8 @@ def main():
     args = ap.parse_args()
     if args.workload == "hard":
         p, s = synth.make_hard_sym(args.n, threads=16)
+    elif args.workload == "heavy":
+        p, s = synth.make_hard_heaviest(args.n, threads=16)
     elif args.workload == "minimal":
         p, s = synth.make_minimal_sym(args.n, threads=16)
     else:
@@ -49,7 +51,8 @@ def main():
                     eng.lib.sdk_debug_dn_ctl(eng.ctx, ctl)
                     c = list(ctl)
                     print(f"  ctl: epoch={c[0]} delivered={c[1]} items={c[2]} nrec={c[3]} exit_all={c[4]} "
-                          f"parts_ended={c[5]} finalized={c[6]} split_boards={eng.get_option(L.SDK_OPT_SPLIT_BOARDS)}",
+                          f"parts_ended={c[5]} finalized={c[6]} err={c[8]} grid={c[10]} helpers={c[11]} "
+                          f"split_boards={eng.get_option(L.SDK_OPT_SPLIT_BOARDS)}",
                           flush=True)
                 ok = (out[st == 1] == s[st == 1]).all()
                 print(f"{args.workload} n={args.n} budget={budget} donate={dn}: kernels {ms:.2f} ms "

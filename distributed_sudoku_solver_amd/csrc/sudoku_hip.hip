@@ -401,7 +401,9 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     return SDK_OK;
 }
 
-// Solve launch.  QUAD LEX solves with SDK_OPT_DONATE run in phases: every board first in
+// Solve launch.  QUAD solves with SDK_OPT_DONATE (LEX, or MRV_UNIQUE: its split phase counts to
+// two completions and re-searches in LEX within the slot, like the plain launch) run in phases:
+// every board first in
 // the plain kernel with at most `split` search nodes (the C4/C2 path is that launch alone);
 // the few boards that need more -- the launch's tail -- are gathered and solved again by
 // solve4_kernel<true> on the full resident grid, where idle waves take subtrees of the
@@ -509,7 +511,8 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     const int64_t dn = donate >= 0 ? donate : (int64_t)c->donate;
     const uint64_t split = dn == 1 ? kDnSplitDefault : (uint64_t)dn;
     const bool two_phase = n > 0 && !count_mode && dn && c->solver == SDK_SOLVER_QUAD &&
-                           eff_order == SDK_ORDER_LEX && d_out && d_status && (node_budget == 0 || node_budget > split) &&
+                           (eff_order == SDK_ORDER_LEX || eff_order == SDK_ORDER_MRV_UNIQUE) && d_out && d_status &&
+                           (node_budget == 0 || node_budget > split) &&
                            (c->dn_max == 0 || (int64_t)n <= c->dn_max);
     c->dn_ran = two_phase;
     if (two_phase) c->dn_err_check = true;

@@ -81,7 +81,7 @@ extern "C" {
                                  /* every node; same answers, fewer search nodes         */
 #define SDK_OPT_XCD_HEADS    14  /* QUAD solver: 1 = one dequeue head per XCD segment of */
                                  /* the batch (default), 0 = one shared head             */
-#define SDK_OPT_DONATE       15  /* QUAD solver, SDK_ORDER_LEX solves: two-phase solve   */
+#define SDK_OPT_DONATE       15  /* QUAD solver (LEX or MRV_UNIQUE order): phased solve  */
                                  /* with subtree donation.  1 (default) or a split       */
                                  /* budget >= 2: every board first gets at most that     */
                                  /* many search nodes (1: 128); the boards that need     */

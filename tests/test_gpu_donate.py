@@ -283,3 +283,23 @@ def test_per_call_donate_leaves_the_context_option(engine):
         assert engine.get_option(L.SDK_OPT_SPLIT_BOARDS) == 0 and (out == s).all()
     finally:
         engine.set_option(L.SDK_OPT_DONATE_MAX, 1 << 19)
+
+
+def test_phased_solve_in_mrv_unique_order(engine):
+    """The phased solve also runs under SDK_ORDER_MRV_UNIQUE (split phase counting to two
+    completions, LEX re-search of multi-solution boards in the slot): heavy unique boards,
+    sparse multi-solution boards with ranges and exact-unsolvable boards give the one-slot LEX
+    answers (the reference's)."""
+    heavy, hs, _ = _heavy_minimal(engine, 8000, 100, 41)
+    puz = np.concatenate([heavy, _random_puzzles(300, 43, 14, 24), _corrupt(heavy[:50], 7)])
+    masks = _masks(len(puz), 44)
+    ref, rst, _, _ = _solve(engine, puz, masks, donate=0, budget=0)
+    engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+    try:
+        out, st, _, donated = _solve(engine, puz, masks, budget=0)
+        split = engine.get_option(L.SDK_OPT_SPLIT_BOARDS)
+    finally:
+        engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
+    assert split > 0 and donated > 0
+    assert (st == rst).all() and (out == ref).all()
+    assert (out[:len(heavy)] == hs).all()

@@ -674,6 +674,11 @@ constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u;
 #ifndef SDK_DN_WAITS
 #define SDK_DN_WAITS 1
 #endif
+// measurement build only: round 3's termination (the `busy` words count idle waves instead, a
+// wave leaves when their sum reaches the grid -- the whole grid must be resident at once)
+#ifndef SDK_DN_EXIT_R03
+#define SDK_DN_EXIT_R03 0
+#endif
 // bound of every wait on another wave, in s_memrealtime ticks (100 MHz): 0.2 s -- a
 // registration is written right after its ticket is drawn and a lock is held for a few
 // hundred cycles, so only a wave that cannot run (a fault, or a preempted queue) gets near it
@@ -753,6 +758,7 @@ static __shared__ DnFin s_dnfin4[4];
 static __shared__ uint32_t s_dnpend4; // bit k: s_dnfin4[k] waits; bit 4 + k: slot k's check is due
 static __shared__ uint32_t s_dnwave4; // bit 0: un-counted from `busy` (idle), bit 1: registered, bits 8..: polls
 static __shared__ uint32_t s_dnepoch4;
+static __shared__ uint32_t s_dnfault4; // DnCtl.fault, read once at entry (registrations must not wait on it)
 static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
 static __shared__ uint32_t s_deq4;     // the wave's dequeue stage (next_board4)
 static __shared__ unsigned long long s_count4;   // count mode: the wave's completions (added to
@@ -850,6 +856,8 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
         tl[k] = ld_agent(&ctl->x[k].reg_tail);
         hd[k] = ld_agent(&ctl->x[k].reg_head);
     }
+    // the error word in the same round trip as the counters (a donor must not wait on it alone)
+    const uint32_t err_seen = SDK_DN_ERRCHECK ? ld_agent(&ctl->err) : 0u;
     uint32_t x = kDnXcds, tail = 0, head = 0;
     for (uint32_t k = 0; k < (uint32_t)kDnXcds && x == kDnXcds; ++k) {
         const uint32_t xx = (blockIdx.x + k) % kDnXcds;
@@ -867,7 +875,7 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     }
     if (x == kDnXcds) return;                                     // no idle wave waits
     if (half_any4(w, w.act && fld_rt(c.E, hi) == 0u)) return;   // only boards with every unit exact
-    if (SDK_DN_ERRCHECK && ld_agent(&ctl->err) != 0u) return;     // a bounded wait ran out: no more donation
+    if (err_seen != 0u) return;                                   // a bounded wait ran out: no more donation
     const uint32_t lvl = d.base;
     uint2* lp = g_stk + (lvl * 2 + hi) * 64 + w.lane;
     const uint2 snap = *lp;
@@ -973,9 +981,9 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
             bool ok = true;
 #if SDK_DN_WAITS
             const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-            while (((e = ld_agent64(reg + t0 + k)) >> 32) != epoch) {
-                if (__builtin_amdgcn_s_memrealtime() - t_start > kDnWaitTicks) {
-                    ok = false;
+            for (uint32_t it = 1; ((e = ld_agent64(reg + t0 + k)) >> 32) != epoch; ++it) {
+                if ((it & 31u) == 0u && __builtin_amdgcn_s_memrealtime() - t_start > kDnWaitTicks) {
+                    ok = false;     // the clock is read every 32 polls: the wait stays a plain poll
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -987,7 +995,10 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
                 atomicOr(&ctl->err, kDnErrReg);
                 break;
             }
-            atomicAdd(&ctl->x[x].busy, 1u);                         // the receiver works from now on
+            if (SDK_DN_EXIT_R03)
+                atomicSub(&ctl->x[x].busy, 1u);
+            else
+                atomicAdd(&ctl->x[x].busy, 1u);                     // the receiver works from now on
             __hip_atomic_store(mbox + (uint32_t)e, ((unsigned long long)epoch << 32) | (i0 + k), __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1188,13 +1199,18 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
     if (!(st & 1u)) {
         // this wave's deliveries were waited for (dn_donate4), so an exit check that sees this
         // decrement sees them (see the hand-off above)
-        if (w.lane == 0) atomicSub(&mx->busy, 1u);
+        if (w.lane == 0) {
+            if (SDK_DN_EXIT_R03)
+                atomicAdd(&mx->busy, 1u);
+            else
+                atomicSub(&mx->busy, 1u);
+        }
         st |= 1u;
     }
     if (!(st & 2u)) {
         if (w.lane == 0) {
             const uint32_t t = atomicAdd(&mx->reg_tail, 1u);
-            if (t < kDnRegX && ld_agent(&ctl->fault) == 0u)
+            if (t < kDnRegX && s_dnfault4 == 0u)
                 __hip_atomic_store(dn_reg4(a) + (size_t)(blockIdx.x % kDnXcds) * kDnRegX + t,
                                    ((unsigned long long)epoch << 32) | blockIdx.x, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -1228,7 +1244,9 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
         busy = wait_done(busy);
         const uint32_t v2 = ld_agent(&ctl->delivered);
         busy = __builtin_amdgcn_readfirstlane(busy);
-        if (busy == 0u && __builtin_amdgcn_readfirstlane(v1) == __builtin_amdgcn_readfirstlane(v2)) {
+        const bool leave = SDK_DN_EXIT_R03 ? busy >= __builtin_amdgcn_readfirstlane(s_dngrid4)
+                                           : (busy == 0u && __builtin_amdgcn_readfirstlane(v1) == __builtin_amdgcn_readfirstlane(v2));
+        if (leave) {
             if (w.lane == 0) atomicAdd(&ctl->exit_all, 1u);
             return 0;
         }
@@ -1805,13 +1823,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         s_dnpend4 = 0u;
         s_dnwave4 = 0u;
         s_dnepoch4 = ld_agent(&a.dn->epoch);
+        s_dnfault4 = ld_agent(&a.dn->fault);
         s_dngrid4 = grid;
         if (blockIdx.x == 0) a.dn->started = grid;    // diagnostics: the waves taking part
         // counted busy before the first dequeue: the add is waited for (its return value used)
         // before the dequeue is issued, so a wave whose dequeue comes up empty after this one's
         // took a board reads this count (see the hand-off above).  No agent-scope fence: a
         // release there writes back the XCD's L2 for every wave of the launch
-#if SDK_DN_WAITS
+#if SDK_DN_EXIT_R03
+#elif SDK_DN_WAITS
         wait_done(atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u));
 #else
         atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u);

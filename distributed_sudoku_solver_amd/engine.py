@@ -249,10 +249,26 @@ class SudokuEngine:
             raise ValueError("budget must be 0 (unlimited) or a positive node count")
         if donate is not None and not 0 <= int(donate) <= (1 << 30):
             raise ValueError("donate must be 0, 1 or a split budget >= 2")
+        if not hasattr(self.lib, "sdk_solve_batch_ex"):
+            # an older library named by SDK_LIB_PATH (dev A/B builds): per-call donate by the option
+            return self._solve_batch_old(boards, masks, out, status, work, budget, donate)
         L.check(self.lib.sdk_solve_batch_ex(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status), _ptr(work),
                                             n, L.SDK_BUDGET_CONTEXT if budget is None else int(budget),
                                             L.SDK_DONATE_CONTEXT if donate is None else int(donate)),
                 "sdk_solve_batch_ex")
+        return out, status, work
+
+    def _solve_batch_old(self, boards, masks, out, status, work, budget, donate):
+        old = self.get_option(L.SDK_OPT_DONATE)
+        if donate is not None:
+            self.set_option(L.SDK_OPT_DONATE, int(donate))
+        try:
+            L.check(self.lib.sdk_solve_batch_budget(self.ctx, _ptr(boards), _ptr(masks), _ptr(out), _ptr(status),
+                                                    _ptr(work), len(boards),
+                                                    L.SDK_BUDGET_CONTEXT if budget is None else int(budget)),
+                    "sdk_solve_batch_budget")
+        finally:
+            self.set_option(L.SDK_OPT_DONATE, old)
         return out, status, work
 
     def expand(self, boards, masks=None, target=64):

@@ -5,7 +5,7 @@ set -o pipefail
 out=gpurun_out/r04g
 mkdir -p $out
 export TMPDIR=/tmp
-for v in base r03; do
+for v in base exit03 exit03all r03; do
   for wl in "heavy 1000 16" "hard 100000 1"; do
     set -- $wl
     SDK_LIB_PATH=$PWD/build/variants/lib_$v.so timeout -k 10 120 python -u tools/dn_diag.py --workload $1 --n $2 \

@@ -621,26 +621,33 @@ struct Args4 : Args2 {
 // input (total 0), or marks the board kDnRetryLex (several completions, or a part that
 // hit the node budget) for a LEX donation launch.
 //
-// Hand-off without a shared queue word: a wave counts itself busy when it starts (before
-// its first dequeue); once its four slots are idle it un-counts itself, registers its id
-// once (reg[reg_tail++]) and polls only its own mailbox.  A donor takes registrations
-// (reg_head moves by compare-and-swap, never past reg_tail), counts each receiver busy
-// again and only then stores the item index in its mailbox, and adds the items to
-// `delivered`.  A wave leaves when no wave is counted busy: no part is running, and no
-// item can be on its way.  Only waves that started are ever counted, so the launch ends
-// whether or not its whole grid was resident at once (a GPU shared with another kernel
-// dispatches the rest of the grid later; those waves find nothing and leave).  The sum of
-// the per-XCD counters is not one snapshot, so the check reads `delivered` before and
-// after it and leaves only if no delivery happened in between (a delivery precedes the
-// donor's own idle decrement).  Every wait on another wave is bounded in time
-// (kDnWaitTicks); one that runs out sets `err` (the host fails the solve with SDK_EHIP)
-// and stops all further donation.  The counters and registries are kept per XCD
-// (workgroup % 8, the dispatch's round robin), each on its own cache line: thousands of
-// waves start and go idle at once, and one shared counter would serialise their atomics;
-// a donor serves its own XCD's idle waves first (the item it writes is then in that XCD's L2).
+// Hand-off without a shared queue word: once its four slots are idle a wave registers its
+// id once (reg[reg_tail++]) and polls only its own mailbox.  A donor takes registrations
+// (reg_head moves by compare-and-swap, never past reg_tail), counts the items in the
+// board record's `open` parts and only then stores each item index in its receiver's
+// mailbox.
+// Termination counts BOARDS, not waves: a board is done when its slot finishes it without
+// having donated, or when the last open part of its record ends (the record is finalized);
+// each adds one to its XCD's `done`.  An idle wave leaves once the eight `done` words add
+// up to the launch's board count.  The words only grow, so a sum of eight separate loads
+// never exceeds the true total: reaching n means every board is done -- no part runs and no
+// item is on its way (an item is counted open before its delivery).  Nothing depends on
+// which waves are resident: a launch whose grid is only partly dispatched (a GPU shared
+// with another kernel) ends when its boards are done, and a wave dispatched after that
+// finds the count complete and leaves.  (Round 4 first counted waves busy at entry and
+// idle when they ran dry, with `delivered` read around the sum as a snapshot check; the
+// idle waves' loads of those hot words slowed the donors' atomics on them, and a 780-board
+// donation launch took 1.75 ms against round 3's 0.89.)
+// Every wait on another wave is bounded in time (kDnWaitTicks); one that runs out sets
+// `err` (the host fails the solve with SDK_EHIP) and stops all further donation; idle
+// waves read `err` every 256th poll and leave once it is set, whatever is still open.  The
+// counters and registries are kept per XCD (workgroup % 8, the dispatch's round robin),
+// each on its own cache line: thousands of waves go idle at once, and one shared counter
+// would serialise their atomics; a donor serves its own XCD's idle waves first (the item it
+// writes is then in that XCD's L2).
 constexpr int kDnXcds = 8;
 struct DnXcd {
-    uint32_t busy;            // waves of this XCD counted working (entry +1, idle -1, delivery +1)
+    uint32_t done;            // boards finished on this XCD
     uint32_t reg_tail;        // registrations of idle waves
     uint32_t reg_head;        // registrations taken by donors (<= reg_tail)
     uint32_t pad[29];
@@ -662,22 +669,13 @@ struct DnCtl {
     DnXcd x[kDnXcds];
 };
 constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u;
-// measurement builds only (tools/build_variant.sh): each round-4 change of the donation kernel
-// alone -- tickets by compare-and-swap, the error-word check before a donation, the waits that
-// order the busy count and `delivered` (and bound the registration wait)
+// measurement builds only (tools/build_variant.sh): round 3's ticket reservation (a plain add,
+// SDK_DN_CAS=0) and no error-word check before a donation (SDK_DN_ERRCHECK=0)
 #ifndef SDK_DN_CAS
 #define SDK_DN_CAS 1
 #endif
 #ifndef SDK_DN_ERRCHECK
 #define SDK_DN_ERRCHECK 1
-#endif
-#ifndef SDK_DN_WAITS
-#define SDK_DN_WAITS 1
-#endif
-// measurement build only: round 3's termination (the `busy` words count idle waves instead, a
-// wave leaves when their sum reaches the grid -- the whole grid must be resident at once)
-#ifndef SDK_DN_EXIT_R03
-#define SDK_DN_EXIT_R03 0
 #endif
 // bound of every wait on another wave, in s_memrealtime ticks (100 MHz): 0.2 s -- a
 // registration is written right after its ticket is drawn and a lock is held for a few
@@ -756,7 +754,7 @@ struct DnFin {
 static __shared__ SlotDn s_dn4[4];    // per slot (half * 2 + slot); referenced by solve4_kernel<true> only
 static __shared__ DnFin s_dnfin4[4];
 static __shared__ uint32_t s_dnpend4; // bit k: s_dnfin4[k] waits; bit 4 + k: slot k's check is due
-static __shared__ uint32_t s_dnwave4; // bit 0: un-counted from `busy` (idle), bit 1: registered, bits 8..: polls
+static __shared__ uint32_t s_dnwave4; // bit 1: registered, bits 8..: polls
 static __shared__ uint32_t s_dnepoch4;
 static __shared__ uint32_t s_dnfault4; // DnCtl.fault, read once at entry (registrations must not wait on it)
 static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
@@ -771,12 +769,6 @@ __device__ __forceinline__ uint32_t fld_rt(uint32_t w, uint32_t hi) {
 }
 __device__ __forceinline__ uint32_t setfld_rt(uint32_t w, uint32_t v, uint32_t hi) {
     return hi ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
-}
-// a value whose memory operation must have completed here (an atomic's return, a load): the
-// compiler waits for it (s_waitcnt) at this point, ordering it before what follows
-__device__ __forceinline__ uint32_t wait_done(uint32_t v) {
-    asm volatile("" : "+v"(v)::"memory");
-    return v;
 }
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -979,7 +971,6 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
             // the registrant writes its entry right after drawing the ticket: a bounded wait
             unsigned long long e;
             bool ok = true;
-#if SDK_DN_WAITS
             const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
             for (uint32_t it = 1; ((e = ld_agent64(reg + t0 + k)) >> 32) != epoch; ++it) {
                 if ((it & 31u) == 0u && __builtin_amdgcn_s_memrealtime() - t_start > kDnWaitTicks) {
@@ -988,25 +979,15 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-#else
-            while (((e = ld_agent64(reg + t0 + k)) >> 32) != epoch) __builtin_amdgcn_s_sleep(1);
-#endif
-            if (!ok) {   // the items left stay undelivered: the solve reports SDK_EHIP
+            if (!ok) {   // the items left stay undelivered (and not open): the solve reports SDK_EHIP
+                atomicSub(&recs[r].open, valid - k);
                 atomicOr(&ctl->err, kDnErrReg);
                 break;
             }
-            if (SDK_DN_EXIT_R03)
-                atomicSub(&ctl->x[x].busy, 1u);
-            else
-                atomicAdd(&ctl->x[x].busy, 1u);                     // the receiver works from now on
             __hip_atomic_store(mbox + (uint32_t)e, ((unsigned long long)epoch << 32) | (i0 + k), __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
-#if SDK_DN_WAITS
-        wait_done(atomicAdd(&ctl->delivered, valid));   // before this wave can count itself idle
-#else
-        atomicAdd(&ctl->delivered, valid);
-#endif
+        atomicAdd(&ctl->delivered, valid);   // diagnostics
     }
     // the level keeps its lower untried digits; with none left it is the donor's no more
     if (stay == 0u) {
@@ -1126,7 +1107,10 @@ __device__ __forceinline__ void dn_finish_part4(const Lane4& w, const Args4& a, 
         if (old == 1u) atomicAdd(&a.dn->finalized, 1u);
     }
     old = half_first4(w, old);
-    if (old == 1u) dn_finalize4(w, a, r);
+    if (old == 1u) {
+        dn_finalize4(w, a, r);
+        if (w.hl == 0) atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].done, 1u);   // the board is done
+    }
 }
 
 // start item `idx` in slot `hi` of this half
@@ -1187,26 +1171,15 @@ __device__ __forceinline__ void dn_check4(const Lane4& w, const Args4& a, const 
     dn_donate4(w, a, s_slot[k], c, k & 1u, pd, g_stk);
 }
 
-// a wave whose four slots are idle: count it idle, register it once, poll its mailbox.
-// Returns 0 to leave (the whole grid idle), 1 to poll again, 2 when an item was started in
-// slot 0 of half 0 (A0 then covers that half).
+// a wave whose four slots are idle: register it once, poll its mailbox.  Returns 0 to leave
+// (every board of the launch done), 1 to poll again, 2 when an item was started in slot 0 of
+// half 0 (A0 then covers that half).
 __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& c, uint64_t& A0, Slot4* s_slot) {
     DnCtl* ctl = a.dn;
     DnXcd* mx = ctl->x + blockIdx.x % kDnXcds;
     uint32_t st = __builtin_amdgcn_readfirstlane(s_dnwave4);
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(s_dnepoch4);
     unsigned long long* mbox = dn_mbox4(a) + blockIdx.x;
-    if (!(st & 1u)) {
-        // this wave's deliveries were waited for (dn_donate4), so an exit check that sees this
-        // decrement sees them (see the hand-off above)
-        if (w.lane == 0) {
-            if (SDK_DN_EXIT_R03)
-                atomicAdd(&mx->busy, 1u);
-            else
-                atomicSub(&mx->busy, 1u);
-        }
-        st |= 1u;
-    }
     if (!(st & 2u)) {
         if (w.lane == 0) {
             const uint32_t t = atomicAdd(&mx->reg_tail, 1u);
@@ -1223,7 +1196,7 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
     const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
     if (mhi == epoch) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the item's words
-        // delivered: the donor counted this wave busy again; its registration is spent
+        // delivered: the item is an open part of its board; the registration is spent
         const uint32_t idx = __builtin_amdgcn_readfirstlane((uint32_t)m);
         if (w.lane == 0) __hip_atomic_store(mbox, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (w.lane == 0) s_dnwave4 = 0u;
@@ -1231,22 +1204,17 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
         A0 = 0x00000000FFFFFFFFull;
         return 2;
     }
-    st += 0x100u;                             // polls; the grid-wide busy count every 16th
+    st += 0x100u;                             // polls; the boards done every 16th
     if (w.lane == 0) s_dnwave4 = st;
     if (((st >> 8) & 15u) == 1u) {
-        // leave when no started wave is busy and no delivery happened while the eight
-        // counters were read (they are not one snapshot: see the hand-off above)
-        // the three reads in this order (each waited for before the next is issued); no agent-
-        // scope acquire: one per check would invalidate the XCD's L2 under the working waves
-        const uint32_t v1 = wait_done(ld_agent(&ctl->delivered));
-        uint32_t busy = 0;
-        for (int k = 0; k < kDnXcds; ++k) busy += ld_agent(&ctl->x[k].busy);
-        busy = wait_done(busy);
-        const uint32_t v2 = ld_agent(&ctl->delivered);
-        busy = __builtin_amdgcn_readfirstlane(busy);
-        const bool leave = SDK_DN_EXIT_R03 ? busy >= __builtin_amdgcn_readfirstlane(s_dngrid4)
-                                           : (busy == 0u && __builtin_amdgcn_readfirstlane(v1) == __builtin_amdgcn_readfirstlane(v2));
-        if (leave) {
+        // leave when the launch's boards are all done (see the hand-off above: eight monotone
+        // words, loaded at once; no agent-scope acquire -- one per check would invalidate the
+        // XCD's L2 under the working waves), or (every 256th poll) a bounded wait ran out
+        uint32_t done = 0;
+#pragma unroll
+        for (int k = 0; k < kDnXcds; ++k) done += ld_agent(&ctl->x[k].done);
+        const bool err = ((st >> 8) & 255u) == 1u && ld_agent(&ctl->err) != 0u;
+        if (__builtin_amdgcn_readfirstlane(done) >= (uint32_t)a.n || __builtin_amdgcn_readfirstlane(err)) {
             if (w.lane == 0) atomicAdd(&ctl->exit_all, 1u);
             return 0;
         }
@@ -1523,6 +1491,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
         if (a.work)
             a.work[b.bidx] = a.work_rounds == 1 ? (uint64_t)(a.iter - b.rstart)
                                                 : (a.work_rounds == 2 ? (uint64_t)b.maxd : b.nodes);
+        if (DN) atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].done, 1u);   // a board that never donated
     }
     next_board4<HI, kFresh4Round && !DN>(w, wr, a, b, c);
 }
@@ -1826,16 +1795,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         s_dnfault4 = ld_agent(&a.dn->fault);
         s_dngrid4 = grid;
         if (blockIdx.x == 0) a.dn->started = grid;    // diagnostics: the waves taking part
-        // counted busy before the first dequeue: the add is waited for (its return value used)
-        // before the dequeue is issued, so a wave whose dequeue comes up empty after this one's
-        // took a board reads this count (see the hand-off above).  No agent-scope fence: a
-        // release there writes back the XCD's L2 for every wave of the launch
-#if SDK_DN_EXIT_R03
-#elif SDK_DN_WAITS
-        wait_done(atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u));
-#else
-        atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].busy, 1u);
-#endif
     }
     {   // segments share the first n - n/128 boards (rounded to whole chunks); the rest is the tail
         a.tail_chunk = max(1u, args.chunk / SDK_SOLVE4_TAIL_CHUNK_DIV);

@@ -302,4 +302,5 @@ def test_phased_solve_in_mrv_unique_order(engine):
         engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
     assert split > 0 and donated > 0
     assert (st == rst).all() and (out == ref).all()
-    assert (out[:len(heavy)] == hs).all()
+    solved = st[:len(heavy)] == 1   # a unique puzzle whose answer lies outside its range has none
+    assert solved.any() and (out[:len(heavy)][solved] == hs[solved]).all()

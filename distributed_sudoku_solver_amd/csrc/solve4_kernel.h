@@ -880,12 +880,14 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     // donor takes belongs to a wave that registered (a plain add with a stale head could
     // pass reg_tail and leave later registrations below it, never served)
     uint32_t t0 = 0, valid = 0;
-#if !SDK_DN_CAS   // round 3's reservation (measurement builds): a stale head can pass reg_tail
+#if SDK_DN_CAS != 1   // 0: round 3's reservation (a stale head can pass reg_tail); 2: the same,
+                     // then the tickets past reg_tail handed back by one compare-and-swap
     if (w.hl == 0) {
         const uint32_t want = min(cnt, tail - head);
         t0 = atomicAdd(&ctl->x[x].reg_head, want);
         const uint32_t tail2 = min(ld_agent(&ctl->x[x].reg_tail), kDnRegX);
         valid = tail2 > t0 ? min(want, tail2 - t0) : 0u;
+        if (SDK_DN_CAS == 2 && valid < want) atomicCAS(&ctl->x[x].reg_head, t0 + want, t0 + valid);
     }
     if (false) {
 #else

@@ -669,10 +669,12 @@ struct DnCtl {
     DnXcd x[kDnXcds];
 };
 constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u;
-// measurement builds only (tools/build_variant.sh): round 3's ticket reservation (a plain add,
-// SDK_DN_CAS=0) and no error-word check before a donation (SDK_DN_ERRCHECK=0)
+// ticket reservation (SDK_DN_CAS): 2 (default) an add, then the tickets past reg_tail handed back
+// by one compare-and-swap; 1 a compare-and-swap loop (never passes reg_tail, but under
+// contention most donation checks fail: 1,300 instead of 1,765 items on the heavy-1000 launch,
+// 1.25 vs 1.08 ms); 0 round 3's add alone.  SDK_DN_ERRCHECK=0: no error-word read (measurement)
 #ifndef SDK_DN_CAS
-#define SDK_DN_CAS 1
+#define SDK_DN_CAS 2
 #endif
 #ifndef SDK_DN_ERRCHECK
 #define SDK_DN_ERRCHECK 1
@@ -848,8 +850,6 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
         tl[k] = ld_agent(&ctl->x[k].reg_tail);
         hd[k] = ld_agent(&ctl->x[k].reg_head);
     }
-    // the error word in the same round trip as the counters (a donor must not wait on it alone)
-    const uint32_t err_seen = SDK_DN_ERRCHECK ? ld_agent(&ctl->err) : 0u;
     uint32_t x = kDnXcds, tail = 0, head = 0;
     for (uint32_t k = 0; k < (uint32_t)kDnXcds && x == kDnXcds; ++k) {
         const uint32_t xx = (blockIdx.x + k) % kDnXcds;
@@ -867,7 +867,6 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     }
     if (x == kDnXcds) return;                                     // no idle wave waits
     if (half_any4(w, w.act && fld_rt(c.E, hi) == 0u)) return;   // only boards with every unit exact
-    if (err_seen != 0u) return;                                   // a bounded wait ran out: no more donation
     const uint32_t lvl = d.base;
     uint2* lp = g_stk + (lvl * 2 + hi) * 64 + w.lane;
     const uint2 snap = *lp;
@@ -875,10 +874,11 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     const int cell = (int)(rec16 & 0x7Fu);
     const uint32_t rest = rec16 >> 7;
     const uint32_t cnt = (uint32_t)__popc(rest);
-    // registrations: tickets t0 .. t0 + valid - 1 are registered idle waves.  reg_head moves
-    // by compare-and-swap and never past a reg_tail value read before, so every ticket a
-    // donor takes belongs to a wave that registered (a plain add with a stale head could
-    // pass reg_tail and leave later registrations below it, never served)
+    // registrations: tickets t0 .. t0 + valid - 1 are registered idle waves.  The add may take
+    // tickets past reg_tail (a stale head): the donor serves only those below the tail it reads
+    // after the add and hands the rest back by one compare-and-swap, which fails only if
+    // another donor took tickets in between -- then those registrations stay unserved (a
+    // wave left idle until the launch ends: throughput, never an answer or termination)
     uint32_t t0 = 0, valid = 0;
 #if SDK_DN_CAS != 1   // 0: round 3's reservation (a stale head can pass reg_tail); 2: the same,
                      // then the tickets past reg_tail handed back by one compare-and-swap
@@ -906,6 +906,10 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
             t = min(ld_agent(&ctl->x[x].reg_tail), kDnRegX);
         }
     }
+    // a bounded wait ran out: no more donation (the error word is read only by a donor that
+    // holds tickets -- in every donation check it cost the heavy-1000 launch ~15 %: the
+    // header line it sits on takes the donors' atomics)
+    if (SDK_DN_ERRCHECK && w.hl == 0 && valid != 0u && ld_agent(&ctl->err) != 0u) valid = 0u;
     t0 = half_first4(w, t0);
     valid = half_first4(w, valid);
     if (valid == 0) return;

@@ -589,6 +589,8 @@ struct Args4 : Args2 {
     // subtree donation (solve4_kernel<true>, see below): control block, then records, items,
     // registrations and mailboxes at fixed offsets
     struct DnCtl* dn;
+    struct SplitSave* save;   // split phase: stacks left for the donation phase (split_save4)
+    uint32_t* save_idx;
 };
 
 // ------------------------------------------------------------------ subtree donation
@@ -652,6 +654,19 @@ struct DnXcd {
     uint32_t reg_head;        // registrations taken by donors (<= reg_tail)
     uint32_t pad[29];
 };
+// Resumed split boards (round 4).  The split phase leaves the stack of a board that reaches
+// the split budget (split_save4); the collect kernel reserves records and items for it, and
+// dn_seed_kernel (sudoku_hip.hip) turns its open subtrees -- the current node's and every
+// level's untried digits -- into items of a board record before the donation launch.  Idle
+// waves take those items from the seed queue first (dn_idle4), so the heavy boards go on
+// from where the split phase left them, spread over the grid, instead of restarting.
+struct DnSeed {
+    uint32_t next;            // seed-queue entries taken by idle waves
+    uint32_t total;           // seed-queue entries (items of the resumed boards)
+    uint32_t boards;          // resumed boards: each ends as a record (counted at the exit)
+    uint32_t res_boards, res_items;   // the collect kernel's reservations (<= kSeedBoards / kSeedItems)
+    uint32_t pad[27];
+};
 struct DnCtl {
     uint32_t epoch;           // launch number (host): mailbox and registration entries carry it
     uint32_t delivered;       // items handed out by the launch
@@ -667,8 +682,9 @@ struct DnCtl {
     uint32_t helpers;         // waves taking part per listed board (SDK_OPT_DONATE_HELPERS), plus 64
     uint32_t pad[20];
     DnXcd x[kDnXcds];
+    DnSeed seed;              // own cache line: idle waves take seed items at the launch's start
 };
-constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u;
+constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u, kDnErrSeed = 4u;
 // ticket reservation (SDK_DN_CAS): 2 (default) an add, then the tickets past reg_tail handed back
 // by one compare-and-swap; 1 a compare-and-swap loop (never passes reg_tail, but under
 // contention most donation checks fail: 1,300 instead of 1,765 items on the heavy-1000 launch,
@@ -722,12 +738,24 @@ struct DnRec {                // one per donating board
     uint8_t owner_sol[96];    // the board's own slot's completion
     uint32_t pad[20];
 };
-static_assert(sizeof(DnItem) == 384 && sizeof(DnRec) == 384 && sizeof(DnCtl) == 128 * (1 + kDnXcds), "donation layout");
+static_assert(sizeof(DnItem) == 384 && sizeof(DnRec) == 384 && sizeof(DnCtl) == 128 * (2 + kDnXcds), "donation layout");
 constexpr size_t kDnRecOffset = sizeof(DnCtl);
 constexpr size_t kDnItemOffset = kDnRecOffset + (size_t)kDnRecs * sizeof(DnRec);
 constexpr size_t kDnRegOffset = kDnItemOffset + (size_t)kDnItems * sizeof(DnItem);
 constexpr size_t kDnMboxOffset = kDnRegOffset + (size_t)kDnReg * 8;
-constexpr size_t kDnBytes = kDnMboxOffset + (size_t)kDnMbox * 8;
+constexpr size_t kDnSeedQOffset = kDnMboxOffset + (size_t)kDnMbox * 8;
+constexpr size_t kDnBytes = kDnSeedQOffset + (size_t)kDnItems * 4;
+constexpr uint32_t kSeedBoards = kDnRecs / 2;   // the other half stays for the launch's own donations
+constexpr uint32_t kSeedItems = kDnItems / 2;
+// the split phase's saved stacks: a board's levels 0..depth-1, the 32 lanes of its half each
+constexpr uint32_t kSaveLv = 16;
+constexpr uint32_t kSaveCap = 8192;
+struct SplitSave {
+    uint32_t count;           // saves claimed (those past kSaveCap are not written)
+    uint32_t pad[31];
+    uint2 hdr[kSaveCap];      // (board, depth)
+    uint2 lv[kSaveCap][kSaveLv][32];
+};
 __device__ __forceinline__ DnRec* dn_recs4(const Args4& a) {
     return reinterpret_cast<DnRec*>(reinterpret_cast<char*>(a.dn) + kDnRecOffset);
 }
@@ -739,6 +767,9 @@ __device__ __forceinline__ unsigned long long* dn_reg4(const Args4& a) {
 }
 __device__ __forceinline__ unsigned long long* dn_mbox4(const Args4& a) {
     return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.dn) + kDnMboxOffset);
+}
+__device__ __forceinline__ uint32_t* dn_seedq4(const Args4& a) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.dn) + kDnSeedQOffset);
 }
 struct SlotDn {
     uint32_t rec, part, base, plen;   // record, part id (item / kDnOwner), first live stack level,
@@ -756,7 +787,9 @@ struct DnFin {
 static __shared__ SlotDn s_dn4[4];    // per slot (half * 2 + slot); referenced by solve4_kernel<true> only
 static __shared__ DnFin s_dnfin4[4];
 static __shared__ uint32_t s_dnpend4; // bit k: s_dnfin4[k] waits; bit 4 + k: slot k's check is due
-static __shared__ uint32_t s_dnwave4; // bit 1: registered, bits 8..: polls
+static __shared__ uint32_t s_dnwave4; // bit 1: registered, bit 2: seed queue drained, bits 8..: polls
+static __shared__ uint32_t s_dntarget4;  // boards of the launch: listed + resumed (the exit count)
+static __shared__ uint32_t s_dnseedn4;   // seed-queue entries
 static __shared__ uint32_t s_dnepoch4;
 static __shared__ uint32_t s_dnfault4; // DnCtl.fault, read once at entry (registrations must not wait on it)
 static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
@@ -1177,15 +1210,29 @@ __device__ __forceinline__ void dn_check4(const Lane4& w, const Args4& a, const 
     dn_donate4(w, a, s_slot[k], c, k & 1u, pd, g_stk);
 }
 
-// a wave whose four slots are idle: register it once, poll its mailbox.  Returns 0 to leave
-// (every board of the launch done), 1 to poll again, 2 when an item was started in slot 0 of
-// half 0 (A0 then covers that half).
+// a wave whose four slots are idle: take an item of a resumed board from the seed queue while
+// there are any, else register once and poll the mailbox.  Returns 0 to leave (every board of
+// the launch done), 1 to poll again, 2 when an item was started in slot 0 of half 0 (A0 then
+// covers that half).
 __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& c, uint64_t& A0, Slot4* s_slot) {
     DnCtl* ctl = a.dn;
     DnXcd* mx = ctl->x + blockIdx.x % kDnXcds;
     uint32_t st = __builtin_amdgcn_readfirstlane(s_dnwave4);
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(s_dnepoch4);
     unsigned long long* mbox = dn_mbox4(a) + blockIdx.x;
+    uint32_t idx = kDnNone;
+    if (!(st & 4u)) {
+        // seed items first (never while registered: registration follows the first empty
+        // claim, and a delivery keeps the drained bit)
+        uint32_t q = 0;
+        if (w.lane == 0) q = atomicAdd(&ctl->seed.next, 1u);
+        q = __builtin_amdgcn_readfirstlane(q);
+        if (q < __builtin_amdgcn_readfirstlane(s_dnseedn4))
+            idx = __builtin_amdgcn_readfirstlane(ld_agent(dn_seedq4(a) + q));
+        else
+            st |= 4u;
+    }
+    if (idx == kDnNone) {
     if (!(st & 2u)) {
         if (w.lane == 0) {
             const uint32_t t = atomicAdd(&mx->reg_tail, 1u);
@@ -1203,9 +1250,12 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
     if (mhi == epoch) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the item's words
         // delivered: the item is an open part of its board; the registration is spent
-        const uint32_t idx = __builtin_amdgcn_readfirstlane((uint32_t)m);
+        idx = __builtin_amdgcn_readfirstlane((uint32_t)m);
         if (w.lane == 0) __hip_atomic_store(mbox, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w.lane == 0) s_dnwave4 = 0u;
+        if (w.lane == 0) s_dnwave4 = 4u;   // not registered; the seed queue was drained before
+    }
+    }
+    if (idx != kDnNone) {
         if (w.half == 0) dn_start_item4(w, a, c, 0u, idx, s_slot);
         A0 = 0x00000000FFFFFFFFull;
         return 2;
@@ -1220,7 +1270,8 @@ __device__ __forceinline__ int dn_idle4(const Lane4& w, const Args4& a, Cells4& 
 #pragma unroll
         for (int k = 0; k < kDnXcds; ++k) done += ld_agent(&ctl->x[k].done);
         const bool err = ((st >> 8) & 255u) == 1u && ld_agent(&ctl->err) != 0u;
-        if (__builtin_amdgcn_readfirstlane(done) >= (uint32_t)a.n || __builtin_amdgcn_readfirstlane(err)) {
+        if (__builtin_amdgcn_readfirstlane(done) >= __builtin_amdgcn_readfirstlane(s_dntarget4) ||
+            __builtin_amdgcn_readfirstlane(err)) {
             if (w.lane == 0) atomicAdd(&ctl->exit_all, 1u);
             return 0;
         }
@@ -1556,6 +1607,33 @@ __device__ __forceinline__ void set_cell4(const Lane4& w, Cells4& c, int cell, u
     c.s2 = k2 ? setfld<HI>(c.s2, d) : c.s2;
 }
 
+#ifndef SDK_SPLIT_SAVE
+#define SDK_SPLIT_SAVE 1   // measurement builds: 0 compiles the save out of the plain kernel
+#endif
+// Split phase of a phased solve: a board that reaches the split budget leaves its DFS stack
+// (levels 0..depth-1, its half's 32 lane words each) for the donation phase, which resumes
+// it (see DnSeed).  Only boards the donation kernel could split (every unit exact), searched
+// in the launch's own order, with no completion met yet and at most kSaveLv levels; the
+// others restart there.
+template <int HI>
+__device__ __forceinline__ void split_save4(const Lane4& w, const Args4& a, const Slot4& b, const Cells4& c,
+                                            const uint2* g_stk) {
+    if (kLds4Levels != 0 || b.count != 0u || b.depth == 0u || b.depth > kSaveLv) return;
+    if (b.order != (a.order == ORDER_LEX ? (uint32_t)ORDER_LEX : (uint32_t)ORDER_MRV)) return;
+    if (half_any4(w, w.act && fld<HI>(c.E) == 0u)) return;
+    uint32_t e = 0;
+    if (w.hl == 0) e = atomicAdd(&a.save->count, 1u);
+    e = half_first4(w, e);
+    if (e >= kSaveCap) return;
+#pragma unroll
+    for (uint32_t l = 0; l < kSaveLv; ++l)
+        if (l < b.depth) a.save->lv[e][l][w.hl] = g_stk[(l * 2 + HI) * 64 + w.lane];
+    if (w.hl == 0) {
+        a.save->hdr[e] = make_uint2(b.bidx, b.depth);
+        a.save_idx[b.bidx] = e;
+    }
+}
+
 // the search step of the board in slot HI after its round ended (bad: contradiction)
 // DFS level record: every lane keeps the level's branch record -- cell | untried
 // digits << 7, uniform in the half -- in the free upper 16 bits of its own snapshot
@@ -1581,6 +1659,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
     int r = bad ? P_CONTRA
                 : (half_any4(w, w.act && (x0 | x1 | x2) != 0u) ? P_OPEN : P_SOLVED);
     if (a.budget && b.nodes > a.budget) {
+        if (!DN && SDK_SPLIT_SAVE && a.save) split_save4<HI>(w, a, b, c, g_stk);
         PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, -2));
         return;
     }
@@ -1751,10 +1830,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     static_assert(!DN || kLds4Levels == 0, "subtree donation needs every DFS level in the global stack");
     uint64_t n = args.n;
     uint32_t grid = gridDim.x;
+    uint32_t resumed = 0;
     if constexpr (DN) {
+        // boards to restart (the list) and resumed boards (seeded before the launch)
+        DnCtl* dn = static_cast<DnCtl*>(args.donate);
         if (args.n_dev) n = min<uint64_t>(*args.n_dev, args.n);
-        grid = (uint32_t)min<uint64_t>(gridDim.x, 64ull + (uint64_t)ld_agent(&static_cast<DnCtl*>(args.donate)->helpers) * n);
-        if (n == 0 || blockIdx.x >= grid) return;
+        resumed = ld_agent(&dn->seed.boards);
+        grid = (uint32_t)min<uint64_t>(gridDim.x, 64ull + (uint64_t)ld_agent(&dn->helpers) * (n + resumed));
+        if (n + resumed == 0 || blockIdx.x >= grid) return;
     }
     __shared__ uint2 s_region[2 * kRegion4];
     __shared__ uint8_t s_in[2 * 2 * 81];
@@ -1793,10 +1876,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     a.count_lim = a.count_stop ? (uint32_t)args.limit : 0x80000000u;
     a.count = args.count;
     a.dn = static_cast<DnCtl*>(args.donate);
+    a.save = static_cast<SplitSave*>(args.save);
+    a.save_idx = args.save_idx;
     if (DN && threadIdx.x < 4) s_dn4[threadIdx.x] = SlotDn{kDnNone, kDnOwner, 0u, 0u};
     if (DN && threadIdx.x == 0) {
         s_dnpend4 = 0u;
-        s_dnwave4 = 0u;
+        s_dnseedn4 = ld_agent(&a.dn->seed.total);
+        s_dnwave4 = s_dnseedn4 == 0u ? 4u : 0u;
+        s_dntarget4 = (uint32_t)n + resumed;
         s_dnepoch4 = ld_agent(&a.dn->epoch);
         s_dnfault4 = ld_agent(&a.dn->fault);
         s_dngrid4 = grid;

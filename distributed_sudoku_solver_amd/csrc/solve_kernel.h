@@ -81,6 +81,9 @@ struct SolveArgs {
     void* donate;              // QUAD solver, LEX solves: subtree-donation area (solve4_kernel.h, DnCtl first)
     const uint32_t* n_dev;     // donation kernel: board count read on the device (a phase's list
                                // length, written by an earlier launch); `n` is then its bound
+    void* save = nullptr;      // QUAD split phase: stacks of boards that reach the split budget
+                               // (solve4_kernel.h SplitSave; nullable)
+    uint32_t* save_idx = nullptr;   // ... and each saved board's entry (by board index)
 };
 
 // per-XCD dequeue: the first n - n/128 boards are cut into kHeads contiguous segments with a

@@ -71,12 +71,40 @@ namespace sdk {
 // first-cell mask) to the list's position in the next phase's dense input: the boards
 // listed are a launch's tail, a few per thousand, so one thread per board does.  n_dev
 // (nullable) bounds n by an earlier list.
+// Resuming (`save` non-null, the split phase's list): a board whose stack the split phase left
+// (SplitSave, validated by its header) goes to the seed list instead -- (board, save entry)
+// pairs after a length word, with the words the records and items it needs reserved in the
+// donation area's DnSeed -- and dn_seed_kernel lists it after the restarted ones; `rcount`
+// counts the restarted boards alone (the donation launch's dequeue).
+struct DnResume {
+    const SplitSave* save;
+    const uint32_t* save_idx;
+    DnCtl* ctl;
+    uint32_t* seeds;          // [0] seeded boards, [1] restarted boards, then (board, entry) pairs
+};
 __global__ void dn_collect_kernel(const int8_t* status, uint64_t n, const uint32_t* n_dev, int8_t code,
                                   uint32_t* list, uint32_t* total, const uint8_t* in, const uint16_t* mask,
-                                  uint64_t in_first, uint64_t in_step, uint8_t* out, uint16_t* out_mask) {
+                                  uint64_t in_first, uint64_t in_step, uint8_t* out, uint16_t* out_mask, DnResume rs) {
     if (n_dev) n = min<uint64_t>(n, *n_dev);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         if (status[i] == code) {
+            if (rs.save) {
+                const uint32_t e = rs.save_idx[i];
+                if (e < min(rs.save->count, kSaveCap) && rs.save->hdr[e].x == (uint32_t)i) {
+                    // items: the deepest level's current digit and every level's untried ones
+                    const uint32_t depth = rs.save->hdr[e].y;
+                    uint32_t items = 1;
+                    for (uint32_t l = 0; l < depth; ++l) items += (uint32_t)__popc(rs.save->lv[e][l][0].y >> 23);
+                    if (atomicAdd(&rs.ctl->seed.res_boards, 1u) < kSeedBoards &&
+                        atomicAdd(&rs.ctl->seed.res_items, items) + items <= kSeedItems) {
+                        const uint32_t s = atomicAdd(rs.seeds, 1u);
+                        rs.seeds[2 + 2 * s] = (uint32_t)i;
+                        rs.seeds[3 + 2 * s] = e;
+                        continue;
+                    }
+                }
+                atomicAdd(rs.seeds + 1, 1u);
+            }
             const uint32_t k = atomicAdd(list, 1u);
             list[1 + k] = (uint32_t)i;
             atomicAdd(total, 1u);
@@ -99,6 +127,8 @@ struct DnPrep {
     uint32_t fault;      // DnCtl.fault (SDK_OPT_DN_FAULT, test only)
     uint32_t helpers;    // DnCtl.helpers (SDK_OPT_DONATE_HELPERS)
     uint32_t* list[2];
+    uint32_t* seeds;     // the seed list's two length words (nullable)
+    uint32_t* save;      // SplitSave::count (nullable)
 };
 __global__ void dn_prep_kernel(DnPrep p) {
     const uint32_t t = threadIdx.x;
@@ -106,6 +136,8 @@ __global__ void dn_prep_kernel(DnPrep p) {
         p.counter[0] = 0;
         p.list[0][0] = 0;
         p.list[1][0] = 0;
+        if (p.seeds) p.seeds[0] = p.seeds[1] = 0;
+        if (p.save) p.save[0] = 0;
     }
     if (p.stat && t < 2) p.stat[t] = 0;
     if (p.heads)
@@ -117,6 +149,84 @@ __global__ void dn_prep_kernel(DnPrep p) {
         for (uint32_t i = t; i < sizeof(DnCtl) / 4; i += blockDim.x)
             if (i != kErr)
                 p.ctl[k][i] = i == kEpoch ? p.epoch[k] : (i == kFault ? p.fault : (i == kHelpers ? p.helpers : 0u));
+}
+// The resumed boards (dn_collect_kernel's seed list), one workgroup of 64 each: listed after the
+// restarted boards (input and mask copied to the dense batch like theirs), a board record with
+// one open part per item, and the items -- each level's snapshot with its branch cell set to
+// one open digit (the deepest level: also the digit it was searching) -- appended to the
+// seed queue, shallowest level first (the largest subtrees start first).
+__global__ void dn_seed_kernel(const uint32_t* seeds, const SplitSave* save, uint32_t* list, uint32_t* total,
+                               const uint8_t* in, const uint16_t* mask, uint64_t in_first, uint64_t in_step,
+                               uint8_t* out, uint16_t* out_mask, DnCtl* ctl) {
+    __shared__ uint32_t sh[4];
+    const uint32_t t = threadIdx.x;
+    DnRec* recs = reinterpret_cast<DnRec*>(reinterpret_cast<char*>(ctl) + kDnRecOffset);
+    DnItem* items = reinterpret_cast<DnItem*>(reinterpret_cast<char*>(ctl) + kDnItemOffset);
+    uint32_t* seedq = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctl) + kDnSeedQOffset);
+    const uint32_t ns = min(seeds[0], kSeedBoards);
+    for (uint32_t s = blockIdx.x; s < ns; s += gridDim.x) {
+        const uint32_t i = seeds[2 + 2 * s], e = seeds[3 + 2 * s];
+        const uint32_t depth = save->hdr[e].y;
+        uint32_t nit = 1;
+        for (uint32_t l = 0; l < depth; ++l) nit += (uint32_t)__popc(save->lv[e][l][0].y >> 23);
+        if (t == 0) {
+            sh[0] = atomicAdd(list, 1u);
+            sh[1] = atomicAdd(&ctl->nrec, 1u);
+            sh[2] = atomicAdd(&ctl->item_alloc, nit);
+            sh[3] = atomicAdd(&ctl->seed.total, nit);
+            atomicAdd(total, 1u);
+        }
+        __syncthreads();
+        const uint32_t k = sh[0], r = sh[1], i0 = sh[2], q0 = sh[3];
+        if (t == 0) list[1 + k] = i;
+        const uint8_t* src = in + (in_first + (uint64_t)i * in_step) * 81;
+        for (uint32_t j = t; j < 81; j += blockDim.x) out[(uint64_t)k * 81 + j] = src[j];
+        if (t == 0 && mask) out_mask[k] = mask[i];
+        DnRec* R = recs + r;
+        if (t == 0) {
+            R->board = k;
+            R->open = nit;
+            R->nhit = R->flags = R->maxd = R->lock = R->version = R->have = 0;
+            R->work = 0;
+            R->total = 0;
+            R->first = kDnNone;
+        }
+        if (t < (uint32_t)kDnList) R->hit[t] = kDnNone;
+        // lane t < 27 of the half owns cells t, t + 27, t + 54: one snapshot word each
+        uint32_t q = 0;
+        for (uint32_t l = 0; l < depth; ++l) {
+            const uint2 hw = save->lv[e][l][0];
+            const uint32_t rec = hw.y >> 16, cell = rec & 0x7Fu;
+            uint32_t digits = rec >> 7;
+            if (l + 1 == depth) {
+                // the digit being searched: the highest one taken (digits go in ascending order)
+                const uint2 cw = save->lv[e][l][cell % 27];
+                const uint32_t third = cell / 27;
+                const uint32_t xc = (third == 0 ? cw.x : (third == 1 ? cw.x >> 16 : cw.y)) & 0x1FFu;
+                const uint32_t taken = xc & ~digits;
+                if (taken) digits |= 1u << (31 - __clz(taken));
+            }
+            const uint2 v = t < 27 ? save->lv[e][l][t] : make_uint2(0, 0);
+            const uint32_t y0 = v.x & 0xFFFFu, y1 = v.x >> 16, y2 = v.y & 0xFFFFu;
+            const bool k0 = cell == t, k1 = cell == t + 27, k2 = cell == t + 54;
+            for (uint32_t g = digits; g; g &= g - 1u, ++q) {
+                const uint32_t dv = (g & (0u - g)) | 0x400u;
+                DnItem* it = items + i0 + q;
+                if (t < 27) it->w[t] = make_uint2((k0 ? dv : y0) | ((k1 ? dv : y1) << 16), k2 ? dv : y2);
+                if (t == 0) {
+                    it->board = k;
+                    it->rec = r;
+                    it->plen = cell + 1u;
+                    seedq[q0 + q] = i0 + q;
+                }
+            }
+        }
+        if (t == 0) {
+            if (q != nit) atomicOr(&ctl->err, kDnErrSeed);   // the reservation and the items disagree
+            atomicAdd(&ctl->seed.boards, 1u);
+        }
+        __syncthreads();
+    }
 }
 __global__ void dn_scatter_kernel(const uint32_t* list, const uint8_t* sub_out, const int8_t* sub_st,
                                   const uint64_t* sub_work, bool depth, uint8_t* out, int8_t* status, uint64_t* work) {
@@ -167,6 +277,9 @@ struct sdk_ctx {
     bool dn_err_check = false;     // a phased solve ran since its control blocks' error words were read
     int dn_fault = 0;              // SDK_OPT_DN_FAULT (test only)
     int dn_helpers = 16;           // SDK_OPT_DONATE_HELPERS: donation-launch waves per listed board (+ 64)
+    int dn_resume = 1;             // SDK_OPT_DONATE_RESUME: split boards resume from their saved stacks
+    bool dn_resume_now = false;    // ... in the phased solve being enqueued (launch_solve)
+    DevBuf dn_save, dn_save_idx, dn_seeds;   // sdk::SplitSave, its entry per board, the seed list
     int dn_exhaustive = 1;         // phase 2 in MRV count-to-2 order (SDK_OPT_DONATE_MODE)
     int64_t dn_max = 1 << 19;      // largest batch solved in phases (SDK_OPT_DONATE_MAX, 0 = any)
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
@@ -360,6 +473,13 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     a.heads = nullptr;
     a.donate = nullptr;
     a.n_dev = nullptr;
+    a.save = nullptr;
+    a.save_idx = nullptr;
+    if (dn_phase == 1 && c->dn_resume_now && four && !count_mode) {
+        // the split phase leaves the stacks of the boards it stops (sdk::split_save4)
+        a.save = c->dn_save.p;
+        a.save_idx = static_cast<uint32_t*>(c->dn_save_idx.p);
+    }
     unsigned grid_used = grid;
     if (four && !count_mode && dn_phase == 2) {
         // subtree donation: idle waves wait for items while any wave of the grid works, so the
@@ -423,25 +543,43 @@ constexpr uint64_t kDnCapBoards = 1ull << 24;
 
 // list the boards of status[0, n) (n bounded by *n_dev when given) that carry `code` into
 // `list` (its length zeroed by the prep launch), copying them to (buf_in, buf_mask)
+// resume: the split phase's list -- boards with saved stacks go to the seed list, and
+// dn_seed_kernel lists them after the restarted ones (donation area 0)
 int dn_collect(sdk_ctx* c, const int8_t* d_status, uint64_t n, const uint32_t* n_dev, int8_t code, DevBuf& list,
                int stat, const uint8_t* d_in, const uint16_t* d_mask, uint64_t in_first, uint64_t in_step,
-               DevBuf& buf_in, DevBuf& buf_mask) {
+               DevBuf& buf_in, DevBuf& buf_mask, bool resume = false) {
     int rc;
     if ((rc = ensure(buf_in, (size_t)n * 81)) || (d_mask && (rc = ensure(buf_mask, (size_t)n * 2)))) return rc;
+    sdk::DnResume rs{};
+    if (resume) {
+        rs.save = static_cast<const sdk::SplitSave*>(c->dn_save.p);
+        rs.save_idx = static_cast<const uint32_t*>(c->dn_save_idx.p);
+        rs.ctl = static_cast<sdk::DnCtl*>(c->dn.p);
+        rs.seeds = static_cast<uint32_t*>(c->dn_seeds.p);
+    }
+    uint32_t* lst = static_cast<uint32_t*>(list.p);
+    uint32_t* total = static_cast<uint32_t*>(c->dn_stat.p) + stat;
+    uint8_t* bin = static_cast<uint8_t*>(buf_in.p);
+    uint16_t* bmask = static_cast<uint16_t*>(d_mask ? buf_mask.p : nullptr);
     sdk::dn_collect_kernel<<<(unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)c->cus * 8)),
-                             256, 0, c->stream>>>(d_status, n, n_dev, code, static_cast<uint32_t*>(list.p),
-                                                  static_cast<uint32_t*>(c->dn_stat.p) + stat, d_in, d_mask, in_first,
-                                                  in_step, static_cast<uint8_t*>(buf_in.p),
-                                                  static_cast<uint16_t*>(d_mask ? buf_mask.p : nullptr));
+                             256, 0, c->stream>>>(d_status, n, n_dev, code, lst, total, d_in, d_mask, in_first, in_step,
+                                                  bin, bmask, rs);
     HIPCALL(hipGetLastError());
+    if (resume) {
+        sdk::dn_seed_kernel<<<(unsigned)std::min<uint64_t>(sdk::kSeedBoards, (uint64_t)c->cus * 4), 64, 0, c->stream>>>(
+            rs.seeds, rs.save, lst, total, d_in, d_mask, in_first, in_step, bin, bmask, rs.ctl);
+        HIPCALL(hipGetLastError());
+    }
     return SDK_OK;
 }
 
 // solve the (at most cap) boards `list` collected into buf_in/buf_mask with the donation
 // kernel (order) in donation area `area`, scatter the answers into (d_out, d_status, d_work)
+// (n_dev: the boards the donation launch dequeues -- the list's length, or with resumed boards
+// the restarted ones alone)
 int dn_resolve(sdk_ctx* c, uint64_t cap, const DevBuf& list, int area, bool has_mask, uint8_t* d_out,
                int8_t* d_status, uint64_t* d_work, int order, int64_t budget, DevBuf& buf_in, DevBuf& buf_mask,
-               DevBuf& buf_out, DevBuf& buf_st, DevBuf& buf_work) {
+               DevBuf& buf_out, DevBuf& buf_st, DevBuf& buf_work, const uint32_t* n_dev = nullptr) {
     int rc;
     if ((rc = ensure(buf_out, (size_t)cap * 81)) || (rc = ensure(buf_st, cap)) ||
         (d_work && (rc = ensure(buf_work, (size_t)cap * 8))))
@@ -453,7 +591,8 @@ int dn_resolve(sdk_ctx* c, uint64_t cap, const DevBuf& list, int area, bool has_
     int8_t* st = static_cast<int8_t*>(buf_st.p);
     uint64_t* work = d_work ? static_cast<uint64_t*>(buf_work.p) : nullptr;
     c->dn_area = static_cast<char*>(c->dn.p) + (size_t)area * sdk::kDnBytes;
-    if ((rc = launch_solve_once(c, in, mask, out, st, work, cap, 0, 0, nullptr, nullptr, 0, 1, order, budget, 2, lst)))
+    if ((rc = launch_solve_once(c, in, mask, out, st, work, cap, 0, 0, nullptr, nullptr, 0, 1, order, budget, 2,
+                                n_dev ? n_dev : lst)))
         return rc;
     if (order == SDK_ORDER_MRV_UNIQUE) {
         // boards with several completions (or undecided): LEX order, donation again
@@ -496,6 +635,13 @@ int dn_prep(sdk_ctx* c, uint64_t cap, bool first_pass) {
     p.helpers = (uint32_t)c->dn_helpers;
     p.list[0] = static_cast<uint32_t*>(c->dn_list.p);
     p.list[1] = static_cast<uint32_t*>(c->dn3_list.p);
+    if (c->dn_resume_now) {
+        if ((rc = ensure(c->dn_save, sizeof(sdk::SplitSave))) || (rc = ensure(c->dn_save_idx, (size_t)cap * 4)) ||
+            (rc = ensure(c->dn_seeds, (2 + 2 * (size_t)sdk::kSeedBoards) * 4)))
+            return rc;
+        p.seeds = static_cast<uint32_t*>(c->dn_seeds.p);
+        p.save = static_cast<uint32_t*>(c->dn_save.p);
+    }
     sdk::dn_prep_kernel<<<1, 256, 0, c->stream>>>(p);
     HIPCALL(hipGetLastError());
     return SDK_OK;
@@ -516,6 +662,9 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
                            (c->dn_max == 0 || (int64_t)n <= c->dn_max);
     c->dn_ran = two_phase;
     if (two_phase) c->dn_err_check = true;
+    // resumed items keep the split phase's branching: LEX items are valid in either donation
+    // order, MRV items only in the exhaustive one (LEX acceptance needs closed prefixes)
+    c->dn_resume_now = two_phase && c->dn_resume && (c->dn_exhaustive || eff_order == SDK_ORDER_LEX);
     if (!two_phase)
         return launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, count_mode, limit, d_count, d_counts,
                                  in_first, in_step, order, budget, 0);
@@ -536,10 +685,11 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
                (rc = launch_solve_once(c, d_in, mask, out, st, work, m, 0, 0, nullptr, nullptr, first, step, order,
                                        (int64_t)split, 1)) ||
                (rc = dn_collect(c, st, m, nullptr, (int8_t)-2, c->dn_list, 0, d_in, mask, first, step, c->dn_in,
-                                c->dn_mask)) ||
+                                c->dn_mask, c->dn_resume_now)) ||
                (rc = dn_resolve(c, m, c->dn_list, 0, mask != nullptr, out, st, work,
                                 c->dn_exhaustive ? SDK_ORDER_MRV_UNIQUE : SDK_ORDER_LEX, (int64_t)node_budget, c->dn_in,
-                                c->dn_mask, c->dn_out, c->dn_st, c->dn_work)));
+                                c->dn_mask, c->dn_out, c->dn_st, c->dn_work,
+                                c->dn_resume_now ? static_cast<uint32_t*>(c->dn_seeds.p) + 1 : nullptr)));
     }
     c->timer_hold = false;
     if (rc) return rc;
@@ -898,6 +1048,8 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             return fail(SDK_EINVAL, "SDK_OPT_DONATED is read-only");
         case SDK_OPT_SPLIT_BOARDS:
             return fail(SDK_EINVAL, "SDK_OPT_SPLIT_BOARDS is read-only");
+        case SDK_OPT_RESUMED:
+            return fail(SDK_EINVAL, "SDK_OPT_RESUMED is read-only");
         case SDK_OPT_LEX_BOARDS:
             return fail(SDK_EINVAL, "SDK_OPT_LEX_BOARDS is read-only");
         case SDK_OPT_DONATE_MAX:
@@ -911,6 +1063,10 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
         case SDK_OPT_DONATE_HELPERS:
             if (value < 1 || value > 4096) return fail(SDK_EINVAL, "SDK_OPT_DONATE_HELPERS must be 1..4096");
             c->dn_helpers = (int)value;
+            return SDK_OK;
+        case SDK_OPT_DONATE_RESUME:
+            if (value != 0 && value != 1) return fail(SDK_EINVAL, "SDK_OPT_DONATE_RESUME must be 0 or 1");
+            c->dn_resume = (int)value;
             return SDK_OK;
         case SDK_OPT_DONATE_MODE:
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "donate mode must be 0 (LEX) or 1 (exhaustive)");
@@ -975,6 +1131,9 @@ int dn_check_error(sdk_ctx* c) {
         HIPCALL(hipMemsetAsync(static_cast<char*>(c->dn.p) + (size_t)k * sdk::kDnBytes + offsetof(sdk::DnCtl, err), 0,
                                sizeof(uint32_t), c->stream));
     HIPCALL(hipStreamSynchronize(c->stream));
+    if (err & sdk::kDnErrSeed)
+        return fail(SDK_EHIP, "donation launch: a resumed board's items disagree with their reservation; the "
+                    "solve's boards are not valid");
     return fail(SDK_EHIP, "donation launch: a bounded wait on another wave ran out (%s%s); the solve's boards are "
                 "not valid", (err & sdk::kDnErrReg) ? "registration entry never written " : "",
                 (err & sdk::kDnErrLock) ? "record lock never released" : "");
@@ -1005,6 +1164,7 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_DONATE_MAX: *value = c->dn_max; return SDK_OK;
         case SDK_OPT_DN_FAULT: *value = c->dn_fault; return SDK_OK;
         case SDK_OPT_DONATE_HELPERS: *value = c->dn_helpers; return SDK_OK;
+        case SDK_OPT_DONATE_RESUME: *value = c->dn_resume; return SDK_OK;
         case SDK_OPT_DONATED: {
             // items handed out by the last phased solve's donation launches (of its last
             // kDnCapBoards-board pass; waits for it on the context's stream)
@@ -1017,6 +1177,18 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
                                        hipMemcpyDeviceToHost, c->stream));
             HIPCALL(hipStreamSynchronize(c->stream));
             *value = (int64_t)h[0].delivered + (int64_t)h[1].delivered;
+            return SDK_OK;
+        }
+        case SDK_OPT_RESUMED: {
+            // boards the last phased solve resumed (donation area 0; waits for the solve)
+            *value = 0;
+            if (!c->dn.p || c->dn_epoch == 0 || !c->dn_ran) return SDK_OK;
+            HIPCALL(hipSetDevice(c->device));
+            sdk::DnSeed h;
+            HIPCALL(hipMemcpyAsync(&h, static_cast<char*>(c->dn.p) + offsetof(sdk::DnCtl, seed), sizeof h,
+                                   hipMemcpyDeviceToHost, c->stream));
+            HIPCALL(hipStreamSynchronize(c->stream));
+            *value = (int64_t)h.boards;
             return SDK_OK;
         }
         case SDK_OPT_TIMER_EVENTS: *value = (int64_t)c->events.size(); return SDK_OK;

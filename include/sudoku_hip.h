@@ -111,6 +111,11 @@ extern "C" {
                                  /* launch is bounded and reports this way)              */
 #define SDK_OPT_DONATE_HELPERS 22 /* waves of a donation launch per board it re-solves   */
                                  /* (plus 64; default 16, at most the resident grid)     */
+#define SDK_OPT_DONATE_RESUME 23 /* 1 (default): a board the split phase stops resumes  */
+                                 /* in the donation launch from its open subtrees (the   */
+                                 /* split phase leaves its DFS stack); 0: it restarts    */
+#define SDK_OPT_RESUMED      24  /* read-only: boards of the last phased solve resumed   */
+                                 /* from their saved stacks (its last pass; waits)       */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

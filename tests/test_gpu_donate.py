@@ -304,3 +304,54 @@ def test_phased_solve_in_mrv_unique_order(engine):
     assert (st == rst).all() and (out == ref).all()
     solved = st[:len(heavy)] == 1   # a unique puzzle whose answer lies outside its range has none
     assert solved.any() and (out[:len(heavy)][solved] == hs[solved]).all()
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+@pytest.mark.parametrize("order", ["lex", "mrv_unique"])
+def test_resumed_split_boards_match_restarted(engine, mode, order):
+    """SDK_OPT_DONATE_RESUME: the boards the split phase stops go on in the donation launch from
+    their saved stacks (the open subtrees of every level as items).  Heavy unique boards, sparse
+    multi-solution boards under first-cell ranges, exact-unsolvable and conflicting boards give
+    the same boards and statuses as restarting them and as one slot per board (LEX: the
+    reference's answer); MRV stacks are resumed only into the exhaustive donation order."""
+    heavy, hs, _ = _heavy_minimal(engine, 8000, 150, 77)
+    puz = np.concatenate([heavy, _random_puzzles(300, 78, 14, 24), _corrupt(heavy[:40], 9)])
+    masks = _masks(len(puz), 79)
+    ref, rst, _, _ = _solve(engine, puz, masks, donate=0, budget=0)
+    ordv = L.SDK_ORDER_LEX if order == "lex" else L.SDK_ORDER_MRV_UNIQUE
+    engine.set_option(L.SDK_OPT_ORDER, ordv)
+    try:
+        res = {}
+        for resume in (1, 0):
+            engine.set_option(L.SDK_OPT_DONATE_RESUME, resume)
+            out, st, _, _ = _solve(engine, puz, masks, budget=0, mode=mode)
+            res[resume] = (out, st, engine.get_option(L.SDK_OPT_RESUMED),
+                           engine.get_option(L.SDK_OPT_SPLIT_BOARDS))
+    finally:
+        engine.set_option(L.SDK_OPT_DONATE_RESUME, 1)
+        engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
+    for resume, (out, st, resumed, split) in res.items():
+        assert (st == rst).all() and (out == ref).all(), f"resume={resume}"
+        assert split > 0
+    assert res[0][2] == 0
+    if order == "lex" or mode == 1:
+        assert res[1][2] > 0
+    else:
+        assert res[1][2] == 0
+
+
+def test_resumed_boards_under_a_budget_and_heaviest(engine):
+    """Resumed boards under a caller's node budget (parts that hit it make the board
+    SDK_BUDGET_HIT unless a completion below it is known, as for a restarted board: never a
+    wrong answer), and the heaviest boards of the hard set resumed at the default split."""
+    heavy, hs, _ = _heavy_minimal(engine, 20000, 1000, 21)
+    for budget in (0, 300, 2000):
+        engine.set_option(L.SDK_OPT_DONATE_RESUME, 1)
+        out, st, _, _ = _solve(engine, heavy, donate=1, budget=budget)
+        resumed = engine.get_option(L.SDK_OPT_RESUMED)
+        ok = st == 1
+        assert (out[ok] == hs[ok]).all()
+        assert ((st == 1) | (st == -2)).all()
+        assert (out[~ok] == heavy[~ok]).all()
+        if budget == 0:
+            assert ok.all() and resumed > 0

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--workload", default="hard")
     ap.add_argument("--budgets", default="0,100000,1000")
     ap.add_argument("--splits", default="1")
+    ap.add_argument("--resume", default="1", help="SDK_OPT_DONATE_RESUME values to run, e.g. 1,0")
     args = ap.parse_args()
     if args.workload == "hard":
         p, s = synth.make_hard_sym(args.n, threads=16)
@@ -32,9 +33,12 @@ def main():
         p, s = synth.make_17clue(args.n, seed=11)
     with SudokuEngine(0) as eng:
         eng.set_option(L.SDK_OPT_TIMING, 1)
-        for budget in [int(x) for x in args.budgets.split(",")]:
-            for dn in [0] + [int(x) for x in args.splits.split(",")]:
+        for budget, dn, rs in [(b, d, r) for b in [int(x) for x in args.budgets.split(",")]
+                               for d in [0] + [int(x) for x in args.splits.split(",")]
+                               for r in ([1] if d == 0 else [int(x) for x in args.resume.split(",")])]:
+            if True:
                 eng.set_option(L.SDK_OPT_DONATE, dn)
+                eng.set_option(L.SDK_OPT_DONATE_RESUME, rs)
                 eng.solve_batch(p[:1024], want_work=True, budget=budget)
                 eng.timer_reset()
                 t0 = time.time()
@@ -55,7 +59,9 @@ def main():
                           f"split_boards={eng.get_option(L.SDK_OPT_SPLIT_BOARDS)}",
                           flush=True)
                 ok = (out[st == 1] == s[st == 1]).all()
-                print(f"{args.workload} n={args.n} budget={budget} donate={dn}: kernels {ms:.2f} ms "
+                resumed = eng.get_option(L.SDK_OPT_RESUMED) if dn else 0
+                print(f"{args.workload} n={args.n} budget={budget} donate={dn} resume={rs} resumed={resumed}: "
+                      f"kernels {ms:.2f} ms "
                       f"wall {wall * 1e3:.1f} ms donated={donated} solved={int((st == 1).sum())} "
                       f"hit={int((st == -2).sum())} nodes sum={int(work.sum())} max={int(work.max())} ok={ok}",
                       flush=True)

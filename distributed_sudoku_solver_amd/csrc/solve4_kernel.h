@@ -1504,8 +1504,16 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
     ++b.bidx;
     if (b.bidx >= b.bend) {
 #endif
-        if (POOL && a.heads) {
-            next_pool4(w, a, b);
+        if constexpr (POOL) {
+            if (a.heads) {
+                next_pool4(w, a, b);
+            } else {
+                uint32_t base = 0;
+                if (w.hl == 0) base = atomicAdd(a.next, a.chunk);
+                base = half_first4(w, base);
+                b.bidx = base;
+                b.bend = (uint32_t)min((uint64_t)base + a.chunk, a.n);
+            }
         } else if (a.heads) {
             // XCD-local segment (see kHeads), then the shared tail: straight-line code, no
             // segment-walking loop (its control flow alone made the allocator spill the
@@ -1681,9 +1689,6 @@ __device__ __forceinline__ void set_cell4(const Lane4& w, Cells4& c, int cell, u
     c.s2 = k2 ? setfld<HI>(c.s2, d) : c.s2;
 }
 
-#ifndef SDK_SPLIT_SAVE
-#define SDK_SPLIT_SAVE 1   // measurement builds: 0 compiles the save out of the plain kernel
-#endif
 // Split phase of a phased solve: a board that reaches the split budget leaves its DFS stack
 // (levels 0..depth-1, its half's 32 lane words each) for the donation phase, which resumes
 // it (see DnSeed).  Only boards the donation kernel could split (every unit exact), searched
@@ -1713,7 +1718,7 @@ __device__ __forceinline__ void split_save4(const Lane4& w, const Args4& a, cons
 // DFS level record: every lane keeps the level's branch record -- cell | untried
 // digits << 7, uniform in the half -- in the free upper 16 bits of its own snapshot
 // word y, so a level is one 8-byte word per lane and needs no shared record array.
-template <bool DN, int HI>
+template <bool DN, int HI, bool SV = false>
 __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c, bool bad,
                                            uint2 (*s_stk)[2][64], uint2* g_stk) {
     ++b.nodes;
@@ -1734,7 +1739,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
     int r = bad ? P_CONTRA
                 : (half_any4(w, w.act && (x0 | x1 | x2) != 0u) ? P_OPEN : P_SOLVED);
     if (a.budget && b.nodes > a.budget) {
-        if (!DN && SDK_SPLIT_SAVE && s_deqp4.save) split_save4<HI>(w, a, b, c, g_stk);
+        if (SV) split_save4<HI>(w, a, b, c, g_stk);
         PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, -2));
         return;
     }
@@ -1863,14 +1868,14 @@ backtrack:
 }
 
 // step of slot HI: its state comes from and returns to LDS; returns whether the slot is active
-template <bool DN, int HI>
+template <bool DN, int HI, bool SV = false>
 __device__ __forceinline__ bool step4(const Lane4& wr, const Args4& a, Cells4& c, bool bad, uint2 (*s_stk)[2][64],
                                       uint2* g_stk_all, Slot4* s_slot, uint2* s_region, uint8_t* s_in) {
     const Lane4 w = lane4_fresh(s_region, s_in);
     uint2* g_stk = g_stk_all + (size_t)blockIdx.x * (kMaxDepth * 2 * 64);
     Slot4* p = s_slot + w.half * 2 + HI;
     Slot4 b;
-    PROF4(1 + HI, b = *p; step4_body<DN, HI>(w, wr, a, b, c, bad, s_stk, g_stk); if (w.hl == 0) *p = b);
+    PROF4(1 + HI, b = *p; step4_body<DN, HI, SV>(w, wr, a, b, c, bad, s_stk, g_stk); if (w.hl == 0) *p = b);
     return (b.active & 1u) != 0u;
 }
 
@@ -1895,7 +1900,7 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
 // VGPRs at 5 waves per SIMD keep its round free of scratch reloads (at 6: 48 B/lane spilled)
 #define SDK_SOLVE4_DN_WAVES_PER_EU 5
 #endif
-template <bool DN>
+template <bool DN, bool SV = false>   // SV: the split phase of a phased solve (split_save4)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOLVE4_DN_WAVES_PER_EU : SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {
     // the donation phases are enqueued without the host: their board count comes from the
     // device (the list the previous phase left), and the launch is the full resident grid, of
@@ -1976,7 +1981,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
             DeqP4 q;
             q.seg_head = args.heads ? args.heads + seg * kHeadStride : nullptr;
             q.tail_head = args.heads ? args.heads + kHeads * kHeadStride : nullptr;
-            q.save = DN ? nullptr : static_cast<SplitSave*>(args.save);
+            q.save = SV ? static_cast<SplitSave*>(args.save) : nullptr;
             q.save_idx = args.save_idx;
             q.lo = seg * a.seg_size;
             q.hi = min(q.lo + a.seg_size, a.tail0);
@@ -2031,13 +2036,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         if (E0 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E0))
-                r = step4<DN, 0>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot, s_region, s_in);
+                r = step4<DN, 0, SV>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot, s_region, s_in);
             A0 = (A0 & ~E0) | (__builtin_amdgcn_ballot_w64(r) & E0);
         }
         if (E1 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E1))
-                r = step4<DN, 1>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot, s_region, s_in);
+                r = step4<DN, 1, SV>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot, s_region, s_in);
             A1 = (A1 & ~E1) | (__builtin_amdgcn_ballot_w64(r) & E1);
         }
         if (DN && (E0 | E1) != 0) {

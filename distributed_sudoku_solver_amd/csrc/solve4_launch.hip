@@ -11,6 +11,8 @@ namespace sdk {
 hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream) {
     if (a.donate)
         solve4_kernel<true><<<grid, 64, 0, stream>>>(a);
+    else if (a.save)   // the split phase of a phased solve: saves the stacks it stops
+        solve4_kernel<false, true><<<grid, 64, 0, stream>>>(a);
     else
         solve4_kernel<false><<<grid, 64, 0, stream>>>(a);
     return hipGetLastError();

@@ -334,7 +334,7 @@ def test_resumed_split_boards_match_restarted(engine, mode, order):
         assert (st == rst).all() and (out == ref).all(), f"resume={resume}"
         assert split > 0
     assert res[0][2] == 0
-    if order == "lex" or mode == 1:
+    if order == "mrv_unique" and mode == 1:   # MRV stacks into the exhaustive launch only
         assert res[1][2] > 0
     else:
         assert res[1][2] == 0
@@ -345,10 +345,15 @@ def test_resumed_boards_under_a_budget_and_heaviest(engine):
     SDK_BUDGET_HIT unless a completion below it is known, as for a restarted board: never a
     wrong answer), and the heaviest boards of the hard set resumed at the default split."""
     heavy, hs, _ = _heavy_minimal(engine, 20000, 1000, 21)
-    for budget in (0, 300, 2000):
-        engine.set_option(L.SDK_OPT_DONATE_RESUME, 1)
-        out, st, _, _ = _solve(engine, heavy, donate=1, budget=budget)
-        resumed = engine.get_option(L.SDK_OPT_RESUMED)
+    engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_MRV_UNIQUE)
+    try:
+        runs = []
+        for budget in (0, 300, 2000):
+            out, st, _, _ = _solve(engine, heavy, donate=1, budget=budget)
+            runs.append((budget, out, st, engine.get_option(L.SDK_OPT_RESUMED)))
+    finally:
+        engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
+    for budget, out, st, resumed in runs:
         ok = st == 1
         assert (out[ok] == hs[ok]).all()
         assert ((st == 1) | (st == -2)).all()

@@ -1423,7 +1423,7 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
 }
 
 #ifndef SDK_SOLVE4_WAVE_POOL
-#define SDK_SOLVE4_WAVE_POOL 1
+#define SDK_SOLVE4_WAVE_POOL 0
 #endif
 // Wave-level dequeue (SDK_SOLVE4_WAVE_POOL, per-XCD heads only).  The wave claims a block of
 // a.chunk boards (a.tail_chunk from the shared tail) with ONE atomic and keeps it in LDS; its

@@ -802,6 +802,7 @@ struct DeqP4 {
     struct SplitSave* save;
     uint32_t* save_idx;
     uint32_t lo, hi, sbase, dealt, tail0, chunk, tail_chunk, pad;
+    uint32_t S, sA, sB, nA, nB, slots, pad2[2];   // SDK_SOLVE4_TICKETS: the segment's ticket map
 };
 static __shared__ DeqP4 s_deqp4;
 static __shared__ unsigned long long s_count4;   // count mode: the wave's completions (added to
@@ -1422,6 +1423,9 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
     c.E = setfld<HI>(c.E, exact);
 }
 
+#ifndef SDK_SOLVE4_TICKETS
+#define SDK_SOLVE4_TICKETS 1
+#endif
 #ifndef SDK_SOLVE4_WAVE_POOL
 #define SDK_SOLVE4_WAVE_POOL 0
 #endif
@@ -1484,6 +1488,16 @@ __device__ __forceinline__ void next_pool4(const Lane4& w, const Args4& a, Slot4
 }
 
 constexpr bool kPool4 = SDK_SOLVE4_WAVE_POOL != 0;
+// SDK_SOLVE4_TICKETS: a segment ticket's first board and chunk end (see next_board4), on
+// wave-uniform values
+__device__ __forceinline__ uint32_t tk_off4(uint32_t t, uint32_t nA, uint32_t nB, uint32_t sA, uint32_t sB,
+                                            uint32_t chunk) {
+    return t < nA ? t * chunk : (t < nA + nB ? sA + (t - nA) * 4u : sA + sB + (t - nA - nB) * 2u);
+}
+__device__ __forceinline__ uint32_t tk_end4(uint32_t t, uint32_t off, uint32_t nA, uint32_t nB, uint32_t sA,
+                                            uint32_t sB, uint32_t S, uint32_t chunk) {
+    return t < nA ? min(off + chunk, sA) : (t < nA + nB ? min(off + 4u, sA + sB) : min(off + 2u, S));
+}
 template <int HI, bool FR = false, bool POOL = false>
 __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c) {
 #if SDK_SOLVE4_STATIC == 1   // experiment: boards dealt round robin to the slots, no dequeue atomics
@@ -1530,6 +1544,64 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
             // does not open with every slot's atomic on eight heads (3,584 each at 28 waves per
             // CU); the head counts the chunks after them.  A dealt chunk past the segment says
             // nothing about the other slots' (the wave stage only follows the heads)
+#if SDK_SOLVE4_TICKETS
+            // tickets (round 4): the head counts tickets, one per claim; ticket t is a chunk of
+            // a.chunk boards of the segment, except the last 4 x slots boards, cut into 4-board
+            // chunks, and the last 2 x slots, into 2-board chunks -- so when the segment runs dry
+            // every slot holds at most 2 boards more, not a.chunk (the launch drain: 1.25M
+            // 17-clue boards spent 0.28 of 1.46 ms finishing 8-board chunks, tools/timeline.py).
+            // The map is arithmetic on the ticket: no memory operation beyond the one atomic
+            // the map's constants: per workgroup, at entry (s_deqp4)
+            const uint32_t slots = __builtin_amdgcn_readfirstlane(s_deqp4.slots);   // dealt tickets
+            const uint32_t S = __builtin_amdgcn_readfirstlane(s_deqp4.S);
+            const uint32_t sA = __builtin_amdgcn_readfirstlane(s_deqp4.sA), sB = __builtin_amdgcn_readfirstlane(s_deqp4.sB);
+            const uint32_t nA = __builtin_amdgcn_readfirstlane(s_deqp4.nA), nB = __builtin_amdgcn_readfirstlane(s_deqp4.nB);
+            // both halves' tickets are wave-uniform (SGPRs): the map runs on the scalar unit and
+            // one select per lane picks its half's range (per-lane maps spilled the round)
+            uint32_t t0 = (blockIdx.x / a.nseg) * 4u + HI, t1 = t0 + 2u;
+            // the first call (first_board4, every lane) is the only one with bend 0: uniform
+            const bool dealt_ok = __builtin_amdgcn_readfirstlane(b.bend) == 0u;
+            bool drained = false;
+            if (!dealt_ok) {
+                const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
+                drained = stage != 0u;
+                if (!drained) {
+                    uint32_t v = 0;
+                    if (w.hl == 0) v = atomicAdd(a.heads + seg * kHeadStride, 1u);
+                    t0 = slots + __builtin_amdgcn_readlane(v, 0);
+                    t1 = slots + __builtin_amdgcn_readlane(v, 32);
+                }
+            }
+            if (!drained) {
+                const uint32_t o0 = tk_off4(t0, nA, nB, sA, sB, a.chunk), o1 = tk_off4(t1, nA, nB, sA, sB, a.chunk);
+                const uint32_t e0 = tk_end4(t0, o0, nA, nB, sA, sB, S, a.chunk), e1 = tk_end4(t1, o1, nA, nB, sA, sB, S, a.chunk);
+                const uint32_t off = w.half ? o1 : o0;
+                base = lo + off;
+                end = lo + (w.half ? e1 : e0);
+                drained = off >= S;
+            }
+            if (dealt_ok && !drained) {
+            } else if (dealt_ok) {
+                // a dealt ticket past the segment says nothing about the other slots'
+                base = (uint32_t)a.n;
+                end = (uint32_t)a.n;
+                drained = false;
+            } else {
+                const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
+                bool empty = stage == 2u;
+                if (drained && !empty) {
+                    if (w.hl == 0) base = atomicAdd(a.heads + kHeads * kHeadStride, a.tail_chunk);
+                    base = a.tail0 + half_first4(w, base);
+                    end = min(base + a.tail_chunk, (uint32_t)a.n);
+                    empty = base >= (uint32_t)a.n;
+                }
+                if (empty) base = (uint32_t)a.n;
+                if (w.hl == 0) atomicMax(&s_deq4, empty ? 2u : (drained ? 1u : 0u));
+            }
+            b.bidx = min(base, (uint32_t)a.n);
+            b.bend = min(end, (uint32_t)a.n);
+            b.active = drained ? 2u : 0u;
+#else
             const uint32_t dealt_base = lo + ((blockIdx.x / a.nseg) * 4u + (uint32_t)w.half * 2u + HI) * a.chunk;
             const bool dealt_ok = b.bend == 0u && dealt_base < hi;
             bool drained = false;
@@ -1559,6 +1631,7 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
             b.bidx = min(base, (uint32_t)a.n);
             b.bend = min(base + (drained ? a.tail_chunk : a.chunk), end);
             b.active = drained ? 2u : 0u;
+#endif
 #if SDK_SOLVE4_TIMELINE
             if (w.hl == 0 && b.bidx < b.bend) TL4(2);
 #endif
@@ -1991,6 +2064,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
             q.chunk = chunk;
             q.tail_chunk = a.tail_chunk;
             q.pad = 0;
+            q.slots = ((grid - seg + a.nseg - 1u) / a.nseg) * 4u;
+            q.S = q.hi > q.lo ? q.hi - q.lo : 0u;
+            const uint32_t sC = min(q.S, 2u * q.slots);
+            q.sB = min(q.S - sC, 4u * q.slots);
+            q.sA = q.S - q.sB - sC;
+            q.nA = (q.sA + chunk - 1u) / chunk;
+            q.nB = (q.sB + 3u) / 4u;
+            q.pad2[0] = q.pad2[1] = 0;
             s_deqp4 = q;
         }
     }

@@ -1424,7 +1424,7 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
 }
 
 #ifndef SDK_SOLVE4_TICKETS
-#define SDK_SOLVE4_TICKETS 1
+#define SDK_SOLVE4_TICKETS 0
 #endif
 #ifndef SDK_SOLVE4_WAVE_POOL
 #define SDK_SOLVE4_WAVE_POOL 0

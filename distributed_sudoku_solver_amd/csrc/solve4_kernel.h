@@ -1580,13 +1580,12 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
                 end = lo + (w.half ? e1 : e0);
                 drained = off >= S;
             }
-            if (dealt_ok && !drained) {
-            } else if (dealt_ok) {
+            if (dealt_ok && drained) {
                 // a dealt ticket past the segment says nothing about the other slots'
                 base = (uint32_t)a.n;
                 end = (uint32_t)a.n;
                 drained = false;
-            } else {
+            } else if (!dealt_ok) {
                 const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
                 bool empty = stage == 2u;
                 if (drained && !empty) {

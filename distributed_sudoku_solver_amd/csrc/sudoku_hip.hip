@@ -420,9 +420,14 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     // profiles/r03/sweep_chunk_r03.log: 1.25M 17-clue 1.489 vs 1.557 ms at 16, 10M 10.01 vs
     // 10.05, 30-clue 1M 0.648 vs 0.676).  Count mode uses single boards (subtrees differ by
     // orders of magnitude).
+    // Round 4, QUAD by batch size (profiles/r04/ab_chunk_by_size_r04u.log, M 17-clue puzzles/s at
+    // chunk 4 / 6 / 8): 1.25M boards 882 / 867 / 862, 2.5M 939 / 958 / 924, 5M 992 / 1000 / 994, 10M
+    // 1026 / 1036 / 1036 -- below 64 boards per slot the launch drain (the last chunks) outweighs
+    // the extra dequeues, so 4; else 6
+    const uint64_t quad_chunk = n < slots * 64 ? 4 : 6;
     const uint32_t chunk = count_mode ? 1u
         : c->solve_chunk ? (uint32_t)c->solve_chunk
-        : (uint32_t)std::min<uint64_t>(per_wave == 4 ? 8 : 16, std::max<uint64_t>(1, n / (slots * 2)));
+        : (uint32_t)std::min<uint64_t>(per_wave == 4 ? quad_chunk : 16, std::max<uint64_t>(1, n / (slots * 2)));
     const uint64_t want = (n + chunk - 1) / chunk;
     const unsigned grid = (unsigned)std::max<uint64_t>(
         1, std::min<uint64_t>((want + per_wave - 1) / per_wave, slots / per_wave));

@@ -276,7 +276,7 @@ struct sdk_ctx {
     bool timer_hold = false;       // a phased solve is being timed as one span
     bool dn_err_check = false;     // a phased solve ran since its control blocks' error words were read
     int dn_fault = 0;              // SDK_OPT_DN_FAULT (test only)
-    int dn_helpers = 16;           // SDK_OPT_DONATE_HELPERS: donation-launch waves per listed board (+ 64)
+    int dn_helpers = 2;            // SDK_OPT_DONATE_HELPERS: donation-launch waves per listed board (+ 64)
     int dn_resume = 1;             // SDK_OPT_DONATE_RESUME: split boards resume from their saved stacks
     bool dn_resume_now = false;    // ... in the phased solve being enqueued (launch_solve)
     DevBuf dn_save, dn_save_idx, dn_seeds;   // sdk::SplitSave, its entry per board, the seed list

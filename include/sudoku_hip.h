@@ -110,7 +110,7 @@ extern "C" {
                                  /* with SDK_EHIP (every wait on another wave inside a   */
                                  /* launch is bounded and reports this way)              */
 #define SDK_OPT_DONATE_HELPERS 22 /* waves of a donation launch per board it re-solves   */
-                                 /* (plus 64; default 16, at most the resident grid)     */
+                                 /* (plus 64; default 2, at most the resident grid)      */
 #define SDK_OPT_DONATE_RESUME 23 /* 1 (default): a board the split phase stops resumes  */
                                  /* in the donation launch from its open subtrees (the   */
                                  /* split phase leaves its DFS stack); 0: it restarts    */

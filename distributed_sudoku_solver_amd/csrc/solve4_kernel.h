@@ -1976,7 +1976,7 @@ template <bool DN, bool SV = false>   // SV: the split phase of a phased solve (
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOLVE4_DN_WAVES_PER_EU : SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {
     // the donation phases are enqueued without the host: their board count comes from the
     // device (the list the previous phase left), and the launch is the full resident grid, of
-    // which 64 + 16 waves per board take part (a few tail boards do not need thousands of
+    // which 64 + SDK_OPT_DONATE_HELPERS (default 2) waves per board take part (a few tail boards do not need thousands of
     // idle waves registering and polling; none when nothing was listed)
     // dn_donate4 reads and rewrites a donated level in the global stack
     static_assert(!DN || kLds4Levels == 0, "subtree donation needs every DFS level in the global stack");

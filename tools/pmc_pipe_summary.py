@@ -43,8 +43,9 @@ def _name(k):
     return k
 
 
-def load(d, tag, kernel="solve4_kernel<false>"):
-    """{dispatch: {counter: value}} and {dispatch: wall ns} of `kernel` in one pass."""
+def load(d, tag, kernel="solve4_kernel<false"):
+    """{dispatch: {counter: value}} and {dispatch: wall ns} of `kernel` in one pass (a name prefix:
+    the plain instance is solve4_kernel<false> to round 4's split-save instance, <false, false> after)."""
     ctr = defaultdict(lambda: defaultdict(float))
     for r in _rows(d, tag, "*counter_collection.csv"):
         if kernel in r["Kernel_Name"]:

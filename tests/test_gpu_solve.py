@@ -318,8 +318,6 @@ def test_solvers_take_identical_search_paths(engine):
     res = {}
     engine.set_option(L.SDK_OPT_LOCKED, 0)
     engine.set_option(L.SDK_OPT_DONATE, 0)       # one slot per board: per-board counters comparable
-    adapt = engine.get_option(L.SDK_OPT_ADAPT)
-    engine.set_option(L.SDK_OPT_ADAPT, 0)        # no order switch: the other solvers have none
     try:
         for solver in SOLVERS:
             engine.set_option(L.SDK_OPT_SOLVER, solver)
@@ -329,7 +327,6 @@ def test_solvers_take_identical_search_paths(engine):
     finally:
         engine.set_option(L.SDK_OPT_LOCKED, 1)
         engine.set_option(L.SDK_OPT_DONATE, 1)
-        engine.set_option(L.SDK_OPT_ADAPT, adapt)
         engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
         engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
     for kind in (L.SDK_WORK_NODES, L.SDK_WORK_ROUNDS):
@@ -413,11 +410,9 @@ def test_minimal_unique_puzzles_100k(engine):
     sparse = _random_puzzles(2000, 91, 8, 20)             # multi-solution: LEX goes deep
     boards = np.concatenate([p[:20000], sparse, np.zeros((1, 81), np.uint8)])
     ref_out2, ref_st2, _ = O.naive_solve_batch(boards[20000:], budget=20_000_000, threads=16)
-    adapt = engine.get_option(L.SDK_OPT_ADAPT)
     try:
         engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_DEPTH)
         engine.set_option(L.SDK_OPT_DONATE, 0)   # donated parts count depth from their own root
-        engine.set_option(L.SDK_OPT_ADAPT, 0)    # LEX all the way: the deep global-stack path
         for solver in SOLVERS:
             engine.set_option(L.SDK_OPT_SOLVER, solver)
             engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
@@ -429,7 +424,6 @@ def test_minimal_unique_puzzles_100k(engine):
     finally:
         engine.set_option(L.SDK_OPT_WORK_COUNTER, L.SDK_WORK_NODES)
         engine.set_option(L.SDK_OPT_DONATE, 1)
-        engine.set_option(L.SDK_OPT_ADAPT, adapt)
         engine.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX)
         engine.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_QUAD)
 
@@ -559,46 +553,3 @@ def test_frontier_rejected_level_leaves_not_counted(engine):
     for target in (1_000_000, 6_000_000, 30_000_000):
         size, leaves = engine.frontier_build(b14, mode=L.SDK_FRONTIER_COUNT, target=target)
         assert _count_all(engine, size) + leaves == 18_204_270, (target, size, leaves)
-
-
-@pytest.mark.parametrize("k", [1, 6, 40])
-def test_adaptive_order_same_answers(engine, k):
-    """SDK_OPT_ADAPT: a LEX board still open after k search nodes restarts in MRV-unique order
-    (count to two; two completions send it back to LEX for good).  Unique heavy boards,
-    multi-solution boards under first-cell ranges, boards with a given planted twice and the
-    empty board give the boards and statuses of plain LEX (the oracle's on a sample), and
-    the switch happens (the node counts differ)."""
-    hp, hs, _ = synth.load_hard(threads=16)
-    heavy, heavy_s = hp[:3000], hs[:3000]
-    sparse = _random_puzzles(1500, 61, 8, 28)
-    odd = _random_puzzles(400, 62, 20, 45)
-    rng = np.random.default_rng(63)
-    for i in range(len(odd)):      # a given planted twice: refuted at the root (no budget needed)
-        nz = np.flatnonzero(odd[i])
-        if len(nz) >= 2:
-            a, b = rng.choice(nz, 2, replace=False)
-            odd[i, b] = odd[i, a]
-    boards = np.concatenate([heavy, sparse, odd, np.zeros((1, 81), np.uint8)])
-    lo = rng.integers(1, 10, len(boards))
-    masks = np.array([O.range_mask(a, min(10, a + int(rng.integers(1, 10)))) for a in lo], dtype=np.uint16)
-    masks[:len(heavy)] = O.range_mask(1, 10)
-    adapt = engine.get_option(L.SDK_OPT_ADAPT)
-    engine.set_option(L.SDK_OPT_DONATE, 0)
-    res = {}
-    try:
-        for kk in (0, k):
-            engine.set_option(L.SDK_OPT_ADAPT, kk)
-            assert engine.get_option(L.SDK_OPT_ADAPT) == kk
-            res[kk] = engine.solve_batch(boards, masks, want_work=True)
-    finally:
-        engine.set_option(L.SDK_OPT_ADAPT, adapt)
-        engine.set_option(L.SDK_OPT_DONATE, 1)
-    (o0, st0, w0), (o1, st1, w1) = res[0], res[k]
-    assert (st0[:len(heavy)] == 1).all() and (o0[:len(heavy)] == heavy_s).all()
-    assert (st1 == st0).all() and (o1 == o0).all()
-    assert (w1 != w0).any()
-    ref_out, ref_st, _ = O.naive_solve_batch(boards[len(heavy):len(heavy) + 300], masks[len(heavy):len(heavy) + 300],
-                                            budget=20_000_000, threads=8)
-    done = ref_st != -2
-    assert (st1[len(heavy):len(heavy) + 300][done] == ref_st[done]).all()
-    assert (o1[len(heavy):len(heavy) + 300][done] == ref_out[done]).all()

@@ -801,8 +801,7 @@ struct DeqP4 {
     uint32_t* tail_head;
     struct SplitSave* save;
     uint32_t* save_idx;
-    uint32_t lo, hi, sbase, dealt, tail0, chunk, tail_chunk;
-    uint32_t adapt;           // plain kernel, LEX launches: search nodes before a board switches to MRV-unique
+    uint32_t lo, hi, sbase, dealt, tail0, chunk, tail_chunk, pad;
     uint32_t S, sA, sB, nA, nB, slots, pad2[2];   // SDK_SOLVE4_TICKETS: the segment's ticket map
 };
 static __shared__ DeqP4 s_deqp4;
@@ -1424,9 +1423,6 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
     c.E = setfld<HI>(c.E, exact);
 }
 
-#ifndef SDK_SOLVE4_ADAPT
-#define SDK_SOLVE4_ADAPT 1   // the adaptive order switch (SDK_OPT_ADAPT) compiled in
-#endif
 #ifndef SDK_SOLVE4_TICKETS
 #define SDK_SOLVE4_TICKETS 0
 #endif
@@ -1862,25 +1858,13 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
             if (b.order == ORDER_MRV && !a.count_mode) {      // >= 2 completions: lex re-search
                 b.order = ORDER_LEX;
                 b.lim = 1;
-                goto restart;
+                start_board4<HI>(w, a, b, c, false);
+            } else {                                           // found, or the count limit
+                PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, 1));
             }
-            PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, 1));   // found, or the count limit
             return;
         }
         r = P_CONTRA;
-    }
-    if (SDK_SOLVE4_ADAPT && r == P_OPEN && !DN && b.order == ORDER_LEX && !(b.active & 4u)) {
-        // adaptive order (SDK_OPT_ADAPT): a LEX board still open after `adapt` nodes starts over in
-        // MRV-unique order -- it is in the launch's tail, where fewest-candidates branching is
-        // shorter (hard set: max 483 nodes instead of 752); a unique completion is the lex-first
-        // one, two send it back to LEX (bit 2 of `active`: no second switch).  Answers unchanged.
-        const uint32_t ak = __builtin_amdgcn_readfirstlane(s_deqp4.adapt);
-        if (ak != 0u && (uint32_t)b.nodes > ak) {
-            b.order = ORDER_MRV;
-            b.lim = 2;
-            b.active |= 4u;
-            goto restart;
-        }
     }
     if (r == P_OPEN) {
         bool lc = false;
@@ -1918,11 +1902,6 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
 #endif
         return;
     }
-    goto backtrack;
-restart:
-    // one inlined restart for both order switches (a second start_board4 site spilled the round)
-    start_board4<HI>(w, a, b, c, false);
-    return;
 backtrack:
     // contradiction: resume the deepest level with untried digits (a donating part: levels
     // below its first live one were given away)
@@ -2083,7 +2062,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
             q.tail0 = a.tail0;
             q.chunk = chunk;
             q.tail_chunk = a.tail_chunk;
-            q.adapt = DN ? 0u : args.adapt;
+            q.pad = 0;
             q.slots = ((grid - seg + a.nseg - 1u) / a.nseg) * 4u;
             q.S = q.hi > q.lo ? q.hi - q.lo : 0u;
             const uint32_t sC = min(q.S, 2u * q.slots);

@@ -84,7 +84,6 @@ struct SolveArgs {
     void* save = nullptr;      // QUAD split phase: stacks of boards that reach the split budget
                                // (solve4_kernel.h SplitSave; nullable)
     uint32_t* save_idx = nullptr;   // ... and each saved board's entry (by board index)
-    uint32_t adapt = 0;        // QUAD, LEX: nodes before a board switches to MRV-unique (0 = never)
 };
 
 // per-XCD dequeue: the first n - n/128 boards are cut into kHeads contiguous segments with a

@@ -278,7 +278,6 @@ struct sdk_ctx {
     int dn_fault = 0;              // SDK_OPT_DN_FAULT (test only)
     int dn_helpers = 2;            // SDK_OPT_DONATE_HELPERS: donation-launch waves per listed board (+ 64)
     int dn_resume = 1;             // SDK_OPT_DONATE_RESUME: split boards resume from their saved stacks
-    int adapt = 0;                 // SDK_OPT_ADAPT: LEX boards switch to MRV-unique after this many nodes
     bool dn_resume_now = false;    // ... in the phased solve being enqueued (launch_solve)
     DevBuf dn_save, dn_save_idx, dn_seeds;   // sdk::SplitSave, its entry per board, the seed list
     int dn_exhaustive = 1;         // phase 2 in MRV count-to-2 order (SDK_OPT_DONATE_MODE)
@@ -481,11 +480,6 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     a.n_dev = nullptr;
     a.save = nullptr;
     a.save_idx = nullptr;
-    // adaptive order: QUAD LEX launches without a node budget, and the split phase (its budget is
-    // the split's, a board stopped there is re-solved anyway); never under a caller's budget,
-    // whose budget hits must stay those of a LEX search
-    a.adapt = (four && !count_mode && a.order == SDK_ORDER_LEX && dn_phase != 2 &&
-               (node_budget == 0 || dn_phase == 1)) ? (uint32_t)c->adapt : 0u;
     if (dn_phase == 1 && c->dn_resume_now && four && !count_mode) {
         // the split phase leaves the stacks of the boards it stops (sdk::split_save4)
         a.save = c->dn_save.p;
@@ -1081,10 +1075,6 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "SDK_OPT_DONATE_RESUME must be 0 or 1");
             c->dn_resume = (int)value;
             return SDK_OK;
-        case SDK_OPT_ADAPT:
-            if (value < 0 || value > (1 << 30)) return fail(SDK_EINVAL, "SDK_OPT_ADAPT must be 0..2^30");
-            c->adapt = (int)value;
-            return SDK_OK;
         case SDK_OPT_DONATE_MODE:
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "donate mode must be 0 (LEX) or 1 (exhaustive)");
             c->dn_exhaustive = (int)value;
@@ -1182,7 +1172,6 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_DN_FAULT: *value = c->dn_fault; return SDK_OK;
         case SDK_OPT_DONATE_HELPERS: *value = c->dn_helpers; return SDK_OK;
         case SDK_OPT_DONATE_RESUME: *value = c->dn_resume; return SDK_OK;
-        case SDK_OPT_ADAPT: *value = c->adapt; return SDK_OK;
         case SDK_OPT_DONATED: {
             // items handed out by the last phased solve's donation launches (of its last
             // kDnCapBoards-board pass; waits for it on the context's stream)

@@ -116,10 +116,6 @@ extern "C" {
                                  /* split phase leaves its DFS stack); 0: it restarts    */
 #define SDK_OPT_RESUMED      24  /* read-only: boards of the last phased solve resumed   */
                                  /* from their saved stacks (its last pass; waits)       */
-#define SDK_OPT_ADAPT        25  /* QUAD, LEX solves without a node budget (and the      */
-                                 /* split phase): a board still open after this many     */
-                                 /* search nodes restarts in MRV-unique order (same      */
-                                 /* answer, shorter tail on hard batches); 0 = never     */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

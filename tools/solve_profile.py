@@ -30,7 +30,6 @@ ap.add_argument("--donate-mode", type=int, default=-1, help="QUAD: SDK_OPT_DONAT
 ap.add_argument("--donate-max", type=int, default=-1, help="QUAD: SDK_OPT_DONATE_MAX (0: phased at any size)")
 ap.add_argument("--helpers", type=int, default=0, help="QUAD: SDK_OPT_DONATE_HELPERS (waves per tail board)")
 ap.add_argument("--resume", type=int, default=-1, help="QUAD: SDK_OPT_DONATE_RESUME (default: library default)")
-ap.add_argument("--adapt", type=int, default=-1, help="QUAD: SDK_OPT_ADAPT (default: library default)")
 args = ap.parse_args()
 
 if args.workload == "minimal":
@@ -64,8 +63,6 @@ with SudokuEngine(0) as eng:
         eng.set_option(L.SDK_OPT_DONATE_HELPERS, args.helpers)
     if args.resume >= 0:
         eng.set_option(L.SDK_OPT_DONATE_RESUME, args.resume)
-    if args.adapt >= 0:
-        eng.set_option(L.SDK_OPT_ADAPT, args.adapt)
     if args.waves_per_cu:
         eng.set_option(wopt, args.waves_per_cu)
     d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)

@@ -697,6 +697,10 @@ constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u, kDnErrSeed = 4u;
 // registration is written right after its ticket is drawn and a lock is held for a few
 // hundred cycles, so only a wave that cannot run (a fault, or a preempted queue) gets near it
 constexpr uint64_t kDnWaitTicks = 20000000ull;
+#ifndef SDK_DN_HELP_CAP
+#define SDK_DN_HELP_CAP 256
+#endif
+constexpr uint64_t kDnHelpCap = SDK_DN_HELP_CAP;   // listed boards that get helper waves
 constexpr uint32_t kDnItems = 1u << 16;
 constexpr uint32_t kDnRecs = 1u << 14;
 constexpr uint32_t kDnRegX = 1u << 14;        // registrations per XCD
@@ -1988,7 +1992,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         DnCtl* dn = static_cast<DnCtl*>(args.donate);
         if (args.n_dev) n = min<uint64_t>(*args.n_dev, args.n);
         resumed = ld_agent(&dn->seed.boards);
-        grid = (uint32_t)min<uint64_t>(gridDim.x, 64ull + (uint64_t)ld_agent(&dn->helpers) * (n + resumed));
+        // the waves the boards fill (four per wave) and the helpers: SDK_OPT_DONATE_HELPERS per board
+        // for the first kDnHelpCap boards (a long list is mostly light boards: more idle waves only
+        // slow the donors with their polls)
+        const uint64_t nb = n + resumed;
+        grid = (uint32_t)min<uint64_t>(gridDim.x, (nb + 3) / 4 + 64ull +
+                                                      (uint64_t)ld_agent(&dn->helpers) * min<uint64_t>(nb, kDnHelpCap));
         if (n + resumed == 0 || blockIdx.x >= grid) return;
     }
     __shared__ uint2 s_region[2 * kRegion4];

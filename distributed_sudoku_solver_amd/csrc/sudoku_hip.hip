@@ -500,10 +500,13 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
         a.n_dev = n_dev;
         a.chunk = 1;
         a.next = &static_cast<sdk::DnCtl*>(c->dn_area)->next;
-        // the resident grid; the kernel keeps 64 + SDK_OPT_DONATE_HELPERS waves per board of it
+        // the resident grid, at most what the kernel keeps of it for n boards: n / 4 + 64 + helpers x
+        // min(n, kDnHelpCap) (solve4_kernel; the list on the device may be shorter, then it keeps less)
         grid_used = (unsigned)std::max<uint64_t>(
             1, std::min<uint64_t>({(uint64_t)c->cus * (uint64_t)std::min(c->dn_blocks_per_cu, c->waves_per_cu2),
-                                   (uint64_t)sdk::kDnMbox, 64ull + (uint64_t)c->dn_helpers * (uint64_t)n}));
+                                   (uint64_t)sdk::kDnMbox,
+                                   ((uint64_t)n + 3) / 4 + 64ull +
+                                       (uint64_t)c->dn_helpers * std::min<uint64_t>(n, sdk::kDnHelpCap)}));
         if (grid_used > grid) {
             rc = ensure(c->stack, (size_t)grid_used * stack_words * sizeof(uint32_t));
             if (rc) return rc;

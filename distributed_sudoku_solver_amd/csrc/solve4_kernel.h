@@ -796,19 +796,14 @@ static __shared__ uint32_t s_dnepoch4;
 static __shared__ uint32_t s_dnfault4; // DnCtl.fault, read once at entry (registrations must not wait on it)
 static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
 static __shared__ uint32_t s_deq4;     // the wave's dequeue stage (next_board4)
-static __shared__ uint32_t s_pool4[2]; // SDK_SOLVE4_WAVE_POOL: the wave's claimed boards [next, end)
-// the wave's dequeue constants and the split phase's save area, in LDS rather than kernel-argument
-// SGPRs: they are read only when a block is claimed / a board saved, and every SGPR live across
-// the round loop is one the allocator may spill into a VGPR lane (and then a round address to scratch)
-struct DeqP4 {
-    uint32_t* seg_head;
-    uint32_t* tail_head;
+// the split phase's save area (split_save4), in LDS rather than kernel-argument SGPRs: it is read
+// only when a board is saved, and every SGPR live across the round loop is one the allocator may
+// spill into a VGPR lane (and then a round address to scratch)
+struct SaveP4 {
     struct SplitSave* save;
     uint32_t* save_idx;
-    uint32_t lo, hi, sbase, dealt, tail0, chunk, tail_chunk, pad;
-    uint32_t S, sA, sB, nA, nB, slots, pad2[2];   // SDK_SOLVE4_TICKETS: the segment's ticket map
 };
-static __shared__ DeqP4 s_deqp4;
+static __shared__ SaveP4 s_save4;
 static __shared__ unsigned long long s_count4;   // count mode: the wave's completions (added to
                                                  // *count once, at the end: same-address atomics
                                                  // per board serialize at ~10 ns)
@@ -1427,82 +1422,7 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
     c.E = setfld<HI>(c.E, exact);
 }
 
-#ifndef SDK_SOLVE4_TICKETS
-#define SDK_SOLVE4_TICKETS 0
-#endif
-#ifndef SDK_SOLVE4_WAVE_POOL
-#define SDK_SOLVE4_WAVE_POOL 0
-#endif
-// Wave-level dequeue (SDK_SOLVE4_WAVE_POOL, per-XCD heads only).  The wave claims a block of
-// a.chunk boards (a.tail_chunk from the shared tail) with ONE atomic and keeps it in LDS; its
-// four slots take single boards from it.  Against a chunk per slot it makes as many atomics
-// per board, but a slot holds at most one board beyond the one it solves, so the launch's
-// drain -- the slots still busy with their last chunks after the queue ran dry -- shrinks
-// from up to a.chunk boards per slot to about a.chunk / 4 (small shards).
-// The halves needing a board now are the exec mask (one or two); everything else is
-// wave-uniform: pool bounds, stage (s_deq4: 0 dealt block pending, 1 home segment, 2 shared
-// tail, 3 empty) and the one atomic, issued by the first active lane.
-__device__ __forceinline__ void next_pool4(const Lane4& w, const Args4& a, Slot4& b) {
-    const uint64_t need = __builtin_amdgcn_ballot_w64(w.hl == 0);
-    const uint32_t nneed = (uint32_t)__builtin_popcountll(need);
-    const uint32_t rank = (w.half == 1 && (need & 1ull)) ? 1u : 0u;
-    const uint32_t pn = __builtin_amdgcn_readfirstlane(s_pool4[0]), pe = __builtin_amdgcn_readfirstlane(s_pool4[1]);
-    uint32_t idx = pn + rank;
-    if (pn + nneed > pe) {
-        // a new block: straight-line, the atomics predicated on the lead lane (a branchy version
-        // made the allocator spill the round's LDS addresses)
-        const uint32_t n = (uint32_t)a.n;
-        const uint32_t chunk = __builtin_amdgcn_readfirstlane(s_deqp4.chunk);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane(s_deqp4.hi);
-        const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
-        const bool lead = (uint32_t)w.lane == __builtin_amdgcn_readfirstlane((uint32_t)w.lane);
-        // the segment's first blocks are dealt, one per workgroup, without an atomic
-        const uint32_t d = __builtin_amdgcn_readfirstlane(s_deqp4.dealt);
-        const bool dealt_ok = stage == 0u && d < hi;
-        const bool try_seg = !dealt_ok && stage <= 1u;
-        uint32_t v = 0;
-        if (lead && try_seg) v = atomicAdd(s_deqp4.seg_head, chunk);
-        const uint32_t sb = __builtin_amdgcn_readfirstlane(s_deqp4.sbase) + __builtin_amdgcn_readfirstlane(v);
-        const bool seg_ok = try_seg && sb < hi;
-        const bool try_tail = !dealt_ok && !seg_ok && stage <= 2u;
-        const uint32_t tchunk = __builtin_amdgcn_readfirstlane(s_deqp4.tail_chunk);
-        uint32_t v2 = 0;
-        if (lead && try_tail) v2 = atomicAdd(s_deqp4.tail_head, tchunk);
-        const uint32_t tb = __builtin_amdgcn_readfirstlane(s_deqp4.tail0) + __builtin_amdgcn_readfirstlane(v2);
-        const bool tail_ok = try_tail && tb < n;
-        const uint32_t g0 = dealt_ok ? d : (seg_ok ? sb : (tail_ok ? tb : n));
-        const uint32_t g1 = dealt_ok ? min(d + chunk, hi)
-                                     : (seg_ok ? min(sb + chunk, hi) : (tail_ok ? min(tb + tchunk, n) : n));
-        s_deq4 = (dealt_ok || seg_ok) ? 1u : (tail_ok ? 2u : 3u);
-        // what is left of the old block goes first (less than the halves need), then the new one
-        const uint32_t left = pe - pn;
-        const uint32_t j = g0 + rank - left;
-        idx = rank < left ? idx : (j < g1 ? j : n);
-        s_pool4[0] = min(g0 + nneed - left, g1);
-        s_pool4[1] = g1;
-    } else {
-        s_pool4[0] = pn + nneed;
-    }
-    b.bidx = min(idx, (uint32_t)a.n);
-    b.bend = b.bidx + 1u;
-    b.active = 0u;
-#if SDK_SOLVE4_TIMELINE
-    if (w.hl == 0 && b.bidx < (uint32_t)a.n) TL4(2);
-#endif
-}
-
-constexpr bool kPool4 = SDK_SOLVE4_WAVE_POOL != 0;
-// SDK_SOLVE4_TICKETS: a segment ticket's first board and chunk end (see next_board4), on
-// wave-uniform values
-__device__ __forceinline__ uint32_t tk_off4(uint32_t t, uint32_t nA, uint32_t nB, uint32_t sA, uint32_t sB,
-                                            uint32_t chunk) {
-    return t < nA ? t * chunk : (t < nA + nB ? sA + (t - nA) * 4u : sA + sB + (t - nA - nB) * 2u);
-}
-__device__ __forceinline__ uint32_t tk_end4(uint32_t t, uint32_t off, uint32_t nA, uint32_t nB, uint32_t sA,
-                                            uint32_t sB, uint32_t S, uint32_t chunk) {
-    return t < nA ? min(off + chunk, sA) : (t < nA + nB ? min(off + 4u, sA + sB) : min(off + 2u, S));
-}
-template <int HI, bool FR = false, bool POOL = false>
+template <int HI, bool FR = false>
 __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c) {
 #if SDK_SOLVE4_STATIC == 1   // experiment: boards dealt round robin to the slots, no dequeue atomics
     b.bidx = b.bend == 0u ? blockIdx.x * 4u + (uint32_t)w.half * 2u + HI : b.bidx + gridDim.x * 4u;
@@ -1522,17 +1442,7 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
     ++b.bidx;
     if (b.bidx >= b.bend) {
 #endif
-        if constexpr (POOL) {
-            if (a.heads) {
-                next_pool4(w, a, b);
-            } else {
-                uint32_t base = 0;
-                if (w.hl == 0) base = atomicAdd(a.next, a.chunk);
-                base = half_first4(w, base);
-                b.bidx = base;
-                b.bend = (uint32_t)min((uint64_t)base + a.chunk, a.n);
-            }
-        } else if (a.heads) {
+        if (a.heads) {
             // XCD-local segment (see kHeads), then the shared tail: straight-line code, no
             // segment-walking loop (its control flow alone made the allocator spill the
             // round's LDS addresses at 72 VGPRs)
@@ -1548,63 +1458,6 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
             // does not open with every slot's atomic on eight heads (3,584 each at 28 waves per
             // CU); the head counts the chunks after them.  A dealt chunk past the segment says
             // nothing about the other slots' (the wave stage only follows the heads)
-#if SDK_SOLVE4_TICKETS
-            // tickets (round 4): the head counts tickets, one per claim; ticket t is a chunk of
-            // a.chunk boards of the segment, except the last 4 x slots boards, cut into 4-board
-            // chunks, and the last 2 x slots, into 2-board chunks -- so when the segment runs dry
-            // every slot holds at most 2 boards more, not a.chunk (the launch drain: 1.25M
-            // 17-clue boards spent 0.28 of 1.46 ms finishing 8-board chunks, tools/timeline.py).
-            // The map is arithmetic on the ticket: no memory operation beyond the one atomic
-            // the map's constants: per workgroup, at entry (s_deqp4)
-            const uint32_t slots = __builtin_amdgcn_readfirstlane(s_deqp4.slots);   // dealt tickets
-            const uint32_t S = __builtin_amdgcn_readfirstlane(s_deqp4.S);
-            const uint32_t sA = __builtin_amdgcn_readfirstlane(s_deqp4.sA), sB = __builtin_amdgcn_readfirstlane(s_deqp4.sB);
-            const uint32_t nA = __builtin_amdgcn_readfirstlane(s_deqp4.nA), nB = __builtin_amdgcn_readfirstlane(s_deqp4.nB);
-            // both halves' tickets are wave-uniform (SGPRs): the map runs on the scalar unit and
-            // one select per lane picks its half's range (per-lane maps spilled the round)
-            uint32_t t0 = (blockIdx.x / a.nseg) * 4u + HI, t1 = t0 + 2u;
-            // the first call (first_board4, every lane) is the only one with bend 0: uniform
-            const bool dealt_ok = __builtin_amdgcn_readfirstlane(b.bend) == 0u;
-            bool drained = false;
-            if (!dealt_ok) {
-                const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
-                drained = stage != 0u;
-                if (!drained) {
-                    uint32_t v = 0;
-                    if (w.hl == 0) v = atomicAdd(a.heads + seg * kHeadStride, 1u);
-                    t0 = slots + __builtin_amdgcn_readlane(v, 0);
-                    t1 = slots + __builtin_amdgcn_readlane(v, 32);
-                }
-            }
-            if (!drained) {
-                const uint32_t o0 = tk_off4(t0, nA, nB, sA, sB, a.chunk), o1 = tk_off4(t1, nA, nB, sA, sB, a.chunk);
-                const uint32_t e0 = tk_end4(t0, o0, nA, nB, sA, sB, S, a.chunk), e1 = tk_end4(t1, o1, nA, nB, sA, sB, S, a.chunk);
-                const uint32_t off = w.half ? o1 : o0;
-                base = lo + off;
-                end = lo + (w.half ? e1 : e0);
-                drained = off >= S;
-            }
-            if (dealt_ok && drained) {
-                // a dealt ticket past the segment says nothing about the other slots'
-                base = (uint32_t)a.n;
-                end = (uint32_t)a.n;
-                drained = false;
-            } else if (!dealt_ok) {
-                const uint32_t stage = __builtin_amdgcn_readfirstlane(s_deq4);
-                bool empty = stage == 2u;
-                if (drained && !empty) {
-                    if (w.hl == 0) base = atomicAdd(a.heads + kHeads * kHeadStride, a.tail_chunk);
-                    base = a.tail0 + half_first4(w, base);
-                    end = min(base + a.tail_chunk, (uint32_t)a.n);
-                    empty = base >= (uint32_t)a.n;
-                }
-                if (empty) base = (uint32_t)a.n;
-                if (w.hl == 0) atomicMax(&s_deq4, empty ? 2u : (drained ? 1u : 0u));
-            }
-            b.bidx = min(base, (uint32_t)a.n);
-            b.bend = min(end, (uint32_t)a.n);
-            b.active = drained ? 2u : 0u;
-#else
             const uint32_t dealt_base = lo + ((blockIdx.x / a.nseg) * 4u + (uint32_t)w.half * 2u + HI) * a.chunk;
             const bool dealt_ok = b.bend == 0u && dealt_base < hi;
             bool drained = false;
@@ -1634,7 +1487,6 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
             b.bidx = min(base, (uint32_t)a.n);
             b.bend = min(base + (drained ? a.tail_chunk : a.chunk), end);
             b.active = drained ? 2u : 0u;
-#endif
 #if SDK_SOLVE4_TIMELINE
             if (w.hl == 0 && b.bidx < b.bend) TL4(2);
 #endif
@@ -1686,7 +1538,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
                 atomicOr(&s_dnpend4, 1u << k);
                 *pd = SlotDn{kDnNone, kDnOwner, 0u, 0u};
             }
-            next_board4<HI, kFresh4Round && !DN, kPool4 && !DN>(w, wr, a, b, c);
+            next_board4<HI, kFresh4Round && !DN>(w, wr, a, b, c);
             return;
         }
     }
@@ -1708,7 +1560,7 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
                                                 : (a.work_rounds == 2 ? (uint64_t)b.maxd : b.nodes);
         if (DN) atomicAdd(&a.dn->x[blockIdx.x % kDnXcds].done, 1u);   // a board that never donated
     }
-    next_board4<HI, kFresh4Round && !DN, kPool4 && !DN>(w, wr, a, b, c);
+    next_board4<HI, kFresh4Round && !DN>(w, wr, a, b, c);
 }
 
 __device__ __forceinline__ uint32_t branch_key4(uint32_t x, uint32_t s, int cell, int order) {
@@ -1776,7 +1628,7 @@ __device__ __forceinline__ void split_save4(const Lane4& w, const Args4& a, cons
     if (kLds4Levels != 0 || b.count != 0u || b.depth == 0u || b.depth > kSaveLv) return;
     if (b.order != (a.order == ORDER_LEX ? (uint32_t)ORDER_LEX : (uint32_t)ORDER_MRV)) return;
     if (half_any4(w, w.act && fld<HI>(c.E) == 0u)) return;
-    SplitSave* sv = s_deqp4.save;
+    SplitSave* sv = s_save4.save;
     uint32_t e = 0;
     if (w.hl == 0) e = atomicAdd(&sv->count, 1u);
     e = half_first4(w, e);
@@ -1786,7 +1638,7 @@ __device__ __forceinline__ void split_save4(const Lane4& w, const Args4& a, cons
         if (l < b.depth) sv->lv[e][l][w.hl] = g_stk[(l * 2 + HI) * 64 + w.lane];
     if (w.hl == 0) {
         sv->hdr[e] = make_uint2(b.bidx, b.depth);
-        s_deqp4.save_idx[b.bidx] = e;
+        s_save4.save_idx[b.bidx] = e;
     }
 }
 
@@ -1964,7 +1816,7 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
     b.active = 0;
     b.depth = 0;
     b.count = 0;
-    next_board4<HI, kFresh4Round && !DN, kPool4 && !DN>(w, w, a, b, c);
+    next_board4<HI, kFresh4Round && !DN>(w, w, a, b, c);
     if (w.hl == 0) s_slot[w.half * 2 + HI] = b;
     return (b.active & 1u) != 0u;
 }
@@ -2008,7 +1860,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     init_lane4(w, s_region, s_in);
     if (threadIdx.x == 0) {
         s_deq4 = 0u;
-        s_pool4[0] = s_pool4[1] = 0u;
         s_count4 = 0ull;
     }
 #if SDK_SOLVE4_PROFILE
@@ -2056,32 +1907,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         // every segment needs a workgroup that drains it: fewer segments on a small grid
         a.nseg = min<uint32_t>(kHeads, grid);
         a.seg_size = (a.tail0 + a.nseg - 1) / a.nseg;
-        if (threadIdx.x == 0) {
-            const uint32_t seg = blockIdx.x % a.nseg;
-            const uint32_t chunk = args.chunk;
-            DeqP4 q;
-            q.seg_head = args.heads ? args.heads + seg * kHeadStride : nullptr;
-            q.tail_head = args.heads ? args.heads + kHeads * kHeadStride : nullptr;
-            q.save = SV ? static_cast<SplitSave*>(args.save) : nullptr;
-            q.save_idx = args.save_idx;
-            q.lo = seg * a.seg_size;
-            q.hi = min(q.lo + a.seg_size, a.tail0);
-            q.dealt = q.lo + (blockIdx.x / a.nseg) * chunk;                      // this workgroup's dealt block
-            q.sbase = q.lo + ((grid - seg + a.nseg - 1u) / a.nseg) * chunk;      // the head counts after the dealt ones
-            q.tail0 = a.tail0;
-            q.chunk = chunk;
-            q.tail_chunk = a.tail_chunk;
-            q.pad = 0;
-            q.slots = ((grid - seg + a.nseg - 1u) / a.nseg) * 4u;
-            q.S = q.hi > q.lo ? q.hi - q.lo : 0u;
-            const uint32_t sC = min(q.S, 2u * q.slots);
-            q.sB = min(q.S - sC, 4u * q.slots);
-            q.sA = q.S - q.sB - sC;
-            q.nA = (q.sA + chunk - 1u) / chunk;
-            q.nB = (q.sB + 3u) / 4u;
-            q.pad2[0] = q.pad2[1] = 0;
-            s_deqp4 = q;
-        }
+        if (SV && threadIdx.x == 0) s_save4 = SaveP4{static_cast<SplitSave*>(args.save), args.save_idx};
     }
 
     Cells4 c;

@@ -241,6 +241,12 @@ class BenchStubEngine(OracleEngine):
     def alloc(self, nbytes):
         return _HostBuffer(nbytes)
 
+    def fork(self):
+        """A second context on the same device (bench.py pipelines its passes over them)."""
+        e = BenchStubEngine(self.device)
+        e.opts = dict(self.opts)
+        return e
+
     def solve_batch_dev(self, d_in, d_out, d_st, n, d_mask=None, d_work=None):
         boards = d_in.data[:n * 81].reshape(n, 81)
         out, st, _ = self.O.naive_solve_batch(boards, budget=50_000_000, threads=2)

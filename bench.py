@@ -55,6 +55,9 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="C4: also time the passes alternating over this many engine contexts (batches in "
+                         "flight; 0/1 = skip), reported as `pipelined`")
     ap.add_argument("--workload", choices=["solve17", "solve30"], default="solve17")
     ap.add_argument("--batch", type=int, default=10_000_000, help="C4 puzzles, whole job (sharded over the GPUs)")
     ap.add_argument("--weak-leg", type=int, default=1, help="N > 1: also time --batch puzzles per GPU (weak scaling)")
@@ -637,40 +640,64 @@ def launch_ranks(args):
     return max(codes, key=abs)
 
 
-def solve_leg(eng, d, args, puzzles, expected, steps, warmup):
+def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1):
     """Time `steps` sdk_solve_batch_dev passes over this rank's resident slice (barrier +
     device sync on both sides, max over ranks); verify every board afterwards.  Each rank's clock
     runs from the release of the opening barrier to its own device sync at the end, and the job's
     time is the maximum over ranks: the closing barrier's host round trip (a TCP exchange, ~0.1 ms,
-    several % of a 1.25M-board shard's step at 8 GPUs) is not the workload's."""
+    several % of a 1.25M-board shard's step at 8 GPUs) is not the workload's.
+
+    With `contexts` > 1 the passes are issued on that many engine contexts in turn
+    (engine.fork(): each its own HIP stream, dequeue state, DFS stacks and output buffer), so that
+    one pass's launch drain -- the last chunks finishing while most of the GPU idles, ~0.3 ms at
+    every batch size -- overlaps the next pass's start: batches in flight, as a serving node keeps
+    them.  Every pass solves the whole slice; every output buffer is checked.  (The headline uses
+    one context: its per-launch HIP events are then the kernel's own duration, the roofline's
+    denominator; overlapped launches' events also hold their wait for the GPU.)"""
     n = len(puzzles)
+    nctx = max(1, min(int(contexts), max(1, steps)))
+    engines = [eng] + [eng.fork() for _ in range(nctx - 1)]
     d_in = eng.alloc(max(n, 1) * 81)
-    d_out = eng.alloc(max(n, 1) * 81)
-    d_st = eng.alloc(max(n, 1))
+    outs = [(e.alloc(max(n, 1) * 81), e.alloc(max(n, 1))) for e in engines]
     d_in.upload(puzzles)
-    for _ in range(warmup):
-        eng.solve_batch_dev(d_in, d_out, d_st, n)
-    eng.synchronize()
-    eng.timer_reset()
+    for i in range(max(warmup, nctx)):
+        o, st = outs[i % nctx]
+        engines[i % nctx].solve_batch_dev(d_in, o, st, n)
+    for e in engines:
+        e.synchronize()
+        e.timer_reset()
     d.barrier()
-    eng.synchronize()
+    for e in engines:
+        e.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        eng.solve_batch_dev(d_in, d_out, d_st, n)
-    eng.synchronize()
+    for i in range(steps):
+        o, st = outs[i % nctx]
+        engines[i % nctx].solve_batch_dev(d_in, o, st, n)
+    for e in engines:
+        e.synchronize()
     elapsed = time.perf_counter() - t0
     d.barrier()
-    kernel_ms, launches = eng.timer_read()
-    eng.timer_stop()
+    kernel_ms, launches = 0.0, 0
+    for e in engines:
+        ms, nl = e.timer_read()
+        e.timer_stop()
+        kernel_ms += ms
+        launches += nl
     elapsed_max = d.max(elapsed)
+    bad = 0
     out = np.empty((n, 81), np.uint8)
-    st = np.empty(n, np.int8)
-    d_out.download(out)
-    d_st.download(st)
-    bad = int(((out != expected).any(axis=1) | (st != 1)).sum())
+    st_h = np.empty(n, np.int8)
+    for o, st in outs:
+        o.download(out)
+        st.download(st_h)
+        bad += int(((out != expected).any(axis=1) | (st_h != 1)).sum())
     bad_total = int(d.sum(bad))
-    for b in (d_in, d_out, d_st):
-        b.free()
+    d_in.free()
+    for o, st in outs:
+        o.free()
+        st.free()
+    for e in engines[1:]:
+        e.close()
     avg_kernel_s = kernel_ms / 1000.0 / max(launches, 1)
     return elapsed_max, avg_kernel_s, bad_total
 
@@ -868,6 +895,19 @@ def main():
         except Exception as e:  # noqa: BLE001
             result[name] = {"error": f"{type(e).__name__}: {e}"}
         return result[name]
+
+    # ------------------------------------------------ batches in flight
+    if args.pipeline > 1:
+        def _pipelined():
+            steps = max(args.steps, 2 * args.pipeline)
+            p_el, _, p_bad = solve_leg(eng, d, args, puzzles, expected, steps, args.warmup, contexts=args.pipeline)
+            return {"contexts": args.pipeline, "steps": steps, "value": total * steps / p_el, "unit": "puzzles/s",
+                    "ms_per_step": p_el / steps * 1000.0, "vs_single_stream": (total * steps / p_el) / value,
+                    "parity": {"mismatched_boards": p_bad, "checked_boards": total * args.pipeline},
+                    "note": "the same passes issued on that many engine contexts in turn (own HIP stream, "
+                            "dequeue state and output buffer each): one pass's launch drain overlaps the "
+                            "next pass's start; `value` above is one context"}
+        side("pipelined", _pipelined)
 
     # ------------------------------------------------ weak-scaling figure
     if d.world > 1 and args.weak_leg:

@@ -640,7 +640,7 @@ def launch_ranks(args):
     return max(codes, key=abs)
 
 
-def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1):
+def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=True):
     """Time `steps` sdk_solve_batch_dev passes over this rank's resident slice (barrier +
     device sync on both sides, max over ranks); verify every board afterwards.  Each rank's clock
     runs from the release of the opening barrier to its own device sync at the end, and the job's
@@ -665,7 +665,8 @@ def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1):
         engines[i % nctx].solve_batch_dev(d_in, o, st, n)
     for e in engines:
         e.synchronize()
-        e.timer_reset()
+        if timed:          # per-launch HIP events (the roofline's kernel time); off: wall clock only
+            e.timer_reset()
     d.barrier()
     for e in engines:
         e.synchronize()
@@ -679,10 +680,11 @@ def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1):
     d.barrier()
     kernel_ms, launches = 0.0, 0
     for e in engines:
-        ms, nl = e.timer_read()
-        e.timer_stop()
-        kernel_ms += ms
-        launches += nl
+        if timed:
+            ms, nl = e.timer_read()
+            e.timer_stop()
+            kernel_ms += ms
+            launches += nl
     elapsed_max = d.max(elapsed)
     bad = 0
     out = np.empty((n, 81), np.uint8)
@@ -899,8 +901,9 @@ def main():
     # ------------------------------------------------ batches in flight
     if args.pipeline > 1:
         def _pipelined():
-            steps = max(args.steps, 2 * args.pipeline)
-            p_el, _, p_bad = solve_leg(eng, d, args, puzzles, expected, steps, args.warmup, contexts=args.pipeline)
+            steps = max(args.steps, 3 * args.pipeline)
+            p_el, _, p_bad = solve_leg(eng, d, args, puzzles, expected, steps, args.warmup, contexts=args.pipeline,
+                                       timed=False)
             return {"contexts": args.pipeline, "steps": steps, "value": total * steps / p_el, "unit": "puzzles/s",
                     "ms_per_step": p_el / steps * 1000.0, "vs_single_stream": (total * steps / p_el) / value,
                     "parity": {"mismatched_boards": p_bad, "checked_boards": total * args.pipeline},

@@ -233,12 +233,11 @@ def test_frontier_first_solution_matches_reference(engine, solve_cases, target):
     including TASK ranges and unsolvable boards, at several frontier sizes (one test per size:
     ~20 s each on one MI355X, far inside the per-test limit)."""
     from distributed_sudoku_solver_amd.shard import sharded_solve
-    if True:
-        for c in solve_cases[:40]:
-            board = np.array(c["puzzle"], np.uint8)
-            out, st = sharded_solve(engine, board, 0, 1, mask=O.range_mask(*c["range"]), target=target)
-            assert (st == 1) == c["ok"], (c["name"], target)
-            assert out.tolist() == (c["board"] if c["ok"] else c["puzzle"]), (c["name"], target)
+    for c in solve_cases[:40]:
+        board = np.array(c["puzzle"], np.uint8)
+        out, st = sharded_solve(engine, board, 0, 1, mask=O.range_mask(*c["range"]), target=target)
+        assert (st == 1) == c["ok"], (c["name"], target)
+        assert out.tolist() == (c["board"] if c["ok"] else c["puzzle"]), (c["name"], target)
 
 
 def test_frontier_first_solution_random_vs_oracle(engine):

@@ -12,7 +12,7 @@ from distributed_sudoku_solver_amd import SudokuEngine, _lib as L  # noqa: E402
 from distributed_sudoku_solver_amd.shard import sharded_solve, default_target  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
-cases = json.load(open(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "solve_cases.json")))
+cases = json.load(open(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "solve_cases.json")))["cases"]
 with SudokuEngine(0) as eng:
     print("default target", default_target(eng, 1))
     for c in cases[:40]:

@@ -489,6 +489,13 @@ def sharded_solve(engine, board, rank, world, comm=None, mask=None, waves=8, tar
     if world > 1 and comm is None:
         raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
     board = np.ascontiguousarray(board, dtype=np.uint8).reshape(81)
+    if target is None and (board > 9).any():
+        # an out-of-domain given makes its units inexact: sub-boards lex-after the answer can take
+        # exponential refutations, and every board of a scanned chunk is solved to its end
+        # (an empty board plus one inert given: 53 s at the default frontier, 0.3 ms unsplit,
+        # tools/frontier_first_probe.py), so such a board is searched unsplit -- the reference's
+        # own DFS order, one slot
+        target = 1
     size, _ = engine.frontier_build(board, mask=mask, mode=L.SDK_FRONTIER_FIRST,
                                     target=default_target(engine, world) if target is None else target)
     if size == 0:

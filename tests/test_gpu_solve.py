@@ -227,7 +227,7 @@ def test_frontier_count_matches_oracle_and_slices_partition(engine):
 DEMO = "000100000000320000000009000000000070000000000000900000000000900000000003000000000"
 
 
-@pytest.mark.parametrize("target", [1, 50, 0])
+@pytest.mark.parametrize("target", [1, 50, 0, None])
 def test_frontier_first_solution_matches_reference(engine, solve_cases, target):
     """sharded_solve (lex-ordered frontier scan) reproduces every golden solve case,
     including TASK ranges and unsolvable boards, at several frontier sizes (one test per size:
@@ -235,6 +235,8 @@ def test_frontier_first_solution_matches_reference(engine, solve_cases, target):
     from distributed_sudoku_solver_amd.shard import sharded_solve
     for c in solve_cases[:40]:
         board = np.array(c["puzzle"], np.uint8)
+        if target == 0 and (board > 9).any():
+            continue   # forced full frontier on an inexact board: tools/frontier_first_probe.py (53 s)
         out, st = sharded_solve(engine, board, 0, 1, mask=O.range_mask(*c["range"]), target=target)
         assert (st == 1) == c["ok"], (c["name"], target)
         assert out.tolist() == (c["board"] if c["ok"] else c["puzzle"]), (c["name"], target)

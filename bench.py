@@ -615,6 +615,22 @@ def http_leg(requests, api="dht"):
             "reference_note": f"{ref} single node, -d 0, measured in the build container (SURVEY §3.1)"}
 
 
+def _checker_last(result, leg):
+    """The C3 checker leg goes at the END of the line (the driver keeps only
+    the tail of stdout), with its headline figures first in a compact summary."""
+    if leg is None:
+        return
+    result.pop("checker", None)
+    result.pop("checker_summary", None)
+    result["checker"] = leg
+    rf = leg["roofline"]
+    result["checker_summary"] = {"metric": "checker HBM GB/s (C3, 82 algorithmic B per board)",
+                                 "boards_per_s": leg["value"], "avg_kernel_ms": leg["avg_kernel_ms"],
+                                 "achieved_gbps": rf["achieved"], "peak_gbps": rf["peak"], "frac": rf["frac"],
+                                 "mismatched_boards": leg["parity"]["mismatched_boards"],
+                                 "checked_boards": leg["parity"]["checked_boards"]}
+
+
 def launch_ranks(args):
     """`--gpus N` without torchrun: start N rank processes of this script (one per GPU) with
     the torchrun environment, before this process touches any GPU; rank 0 prints the line."""
@@ -873,9 +889,6 @@ def main():
         "parity": {"mismatched_boards": bad_total, "checked_boards": total},
     }
 
-    if checker_leg is not None:
-        result["checker"] = checker_leg
-
     # side legs run under a watchdog: if one stalls (e.g. a collective), rank 0
     # still prints the line with everything measured so far
     import threading
@@ -883,6 +896,7 @@ def main():
     def _watchdog():
         if d.rank == 0:
             result["watchdog"] = f"side legs stopped after {args.leg_timeout} s"
+            _checker_last(result, checker_leg)
             print(json.dumps(result), flush=True)
         os._exit(3 if bad_total else 0)
     dog = threading.Timer(args.leg_timeout, _watchdog)
@@ -967,6 +981,7 @@ def main():
 
     dog.cancel()
     eng.close()
+    _checker_last(result, checker_leg)
     if d.rank == 0:
         print(json.dumps(result), flush=True)
     d.close()

@@ -102,6 +102,9 @@ SIGNATURES = {
     "sdk_frontier_load_dev": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64]),
     "sdk_frontier_refine_range": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "sdk_frontier_refine_head": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                                ctypes.POINTER(ctypes.c_uint64)]),
     "sdk_comm_send_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int]),
     "sdk_comm_recv_dev": (ctypes.c_int, [_vp, _vp, _sz, ctypes.c_int]),
     "sdk_comm_p2p_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _vp]),

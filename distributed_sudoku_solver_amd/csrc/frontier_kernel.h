@@ -21,7 +21,8 @@
 // stop flag from FrontierCtl (frontier_begin/end_kernel update them), so the host
 // enqueues levels without waiting and reads the control block every few levels.
 //   first_hit_kernel  after a batched solve of frontier boards [lo, hi): the
-//                  lowest index whose status is not "no solution" and its board.
+//                  lowest index whose status is not "no solution" (nor "cancelled": above a
+//                  lower hit, kStCancelled) and its board.
 //
 // First-solution mode (keep_leaves): a board that propagates to SOLVED stays in
 // the frontier as its own single child instead of being counted, and the branch
@@ -272,6 +273,9 @@ __global__ __launch_bounds__(256) void gather_boards_kernel(const uint8_t* __res
     }
 }
 
+// the found word of a first-solution scan before its solve launch (no hit yet)
+__global__ void first_init_kernel(long long* found) { *found = 0x7FFFFFFFFFFFFFFFll; }
+
 __global__ __launch_bounds__(256) void first_hit_kernel(const int8_t* __restrict__ status,
                                                         const uint8_t* __restrict__ out, uint64_t n, uint64_t lo,
                                                         long long* found, uint8_t* best) {
@@ -279,7 +283,7 @@ __global__ __launch_bounds__(256) void first_hit_kernel(const int8_t* __restrict
     const int t = threadIdx.x;
     unsigned long long mine = ~0ull;
     for (uint64_t i = t; i < n; i += 256)
-        if (status[i] != 0) { mine = i; break; }
+        if (status[i] != 0 && status[i] != kStCancelled) { mine = i; break; }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) mine = min(mine, (unsigned long long)__shfl_xor(mine, d));
     if ((t & 63) == 0) s_min[t >> 6] = mine;

@@ -804,6 +804,16 @@ struct SaveP4 {
     uint32_t* save_idx;
 };
 static __shared__ SaveP4 s_save4;
+// First-solution scan of a lex-ordered frontier (solve4_kernel<false, false, true>, sdk_frontier_first):
+// frontier board i's completions all precede board i+1's (frontier_kernel.h), so once board i has a
+// completion -- or hit the node budget, which decides the answer just the same (status -2) -- no
+// board above i can matter.  A board that ends with status 1 or -2 lowers the launch's found word
+// to its index (atomicMin); every board polls the word at its first search step and every
+// kFsEvery nodes after it and stops, with status kStCancelled, once it lies above it (the
+// survey's "shards whose index is above the minimum may stop").  Boards below the
+// lowest hit never stop.  The pointer is kept in LDS like the split phase's save area.
+constexpr uint32_t kFsEvery = 8;
+static __shared__ long long* s_found4;
 static __shared__ unsigned long long s_count4;   // count mode: the wave's completions (added to
                                                  // *count once, at the end: same-address atomics
                                                  // per board serialize at ~10 ns)
@@ -1524,7 +1534,7 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
     }
 }
 
-template <bool DN, int HI>
+template <bool DN, int HI, bool FS = false>
 __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c,
                                               int st) {
     if (DN) {
@@ -1553,6 +1563,8 @@ __device__ __forceinline__ void finish_board4(const Lane4& w, const Lane4& wr, c
         dst[w.c0 + 27] = sin[w.c0 + 27];
         dst[w.c0 + 54] = sin[w.c0 + 54];
     }
+    if (FS && w.hl == 0 && (st == 1 || st == -2))   // boards above this one cannot matter any more
+        atomicMin(s_found4, (long long)(a.in_first + (uint64_t)b.bidx * a.in_step));
     if (w.hl == 0) {
         a.status[b.bidx] = (int8_t)st;
         if (a.work)
@@ -1646,7 +1658,7 @@ __device__ __forceinline__ void split_save4(const Lane4& w, const Args4& a, cons
 // DFS level record: every lane keeps the level's branch record -- cell | untried
 // digits << 7, uniform in the half -- in the free upper 16 bits of its own snapshot
 // word y, so a level is one 8-byte word per lane and needs no shared record array.
-template <bool DN, int HI, bool SV = false>
+template <bool DN, int HI, bool SV = false, bool FS = false>
 __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c, bool bad,
                                            uint2 (*s_stk)[2][64], uint2* g_stk) {
     ++b.nodes;
@@ -1654,7 +1666,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
     if (DN) {
         dd = s_dn4[w.half * 2 + HI];
         if (dd.plen & kDnAbort) {     // pruned by dn_check4
-            PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, kDnPruned));
+            PROF4(3, finish_board4<DN, HI, FS>(w, wr, a, b, c, kDnPruned));
             return;
         }
         // every kDnEvery nodes of a LEX solve: prune / donate check after the step (dn_check4)
@@ -1662,13 +1674,25 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
             !a.count_mode && w.hl == 0)
             atomicOr(&s_dnpend4, 16u << (w.half * 2 + HI));
     }
+    if (FS && (b.nodes & (kFsEvery - 1u)) == 1u) {
+        // first-solution scan: stop a board that lies above the lowest hit of the launch (an
+        // agent-scope load: the found word is lowered by atomics from every XCD)
+        bool above = false;
+        if (w.hl == 0)
+            above = (long long)(a.in_first + (uint64_t)b.bidx * a.in_step) >
+                    __hip_atomic_load(s_found4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (half_any4(w, above)) {
+            PROF4(3, finish_board4<DN, HI, FS>(w, wr, a, b, c, kStCancelled));
+            return;
+        }
+    }
     const uint32_t x0 = fld<HI>(c.x0), x1 = fld<HI>(c.x1), x2 = fld<HI>(c.x2);
     const uint32_t s0 = fld<HI>(c.s0), s1 = fld<HI>(c.s1), s2 = fld<HI>(c.s2);
     int r = bad ? P_CONTRA
                 : (half_any4(w, w.act && (x0 | x1 | x2) != 0u) ? P_OPEN : P_SOLVED);
     if (a.budget && b.nodes > a.budget) {
         if (SV) split_save4<HI>(w, a, b, c, g_stk);
-        PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, -2));
+        PROF4(3, finish_board4<DN, HI, FS>(w, wr, a, b, c, -2));
         return;
     }
     if (r == P_SOLVED) {
@@ -1696,7 +1720,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
                     goto backtrack;
                 }
             }
-            PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, 1));   // LEX: the region's first
+            PROF4(3, finish_board4<DN, HI, FS>(w, wr, a, b, c, 1));   // LEX: the region's first
             return;
         } else if (b.count == 1 && w.act && a.out && !SDK_SOLVE4_NO_OUTPUT) {
             uint8_t* dst = a.out + (uint64_t)b.bidx * 81;
@@ -1716,7 +1740,7 @@ __device__ __forceinline__ void step4_body(const Lane4& w, const Lane4& wr, cons
                 b.lim = 1;
                 start_board4<HI>(w, a, b, c, false);
             } else {                                           // found, or the count limit
-                PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, 1));
+                PROF4(3, finish_board4<DN, HI, FS>(w, wr, a, b, c, 1));
             }
             return;
         }
@@ -1762,7 +1786,7 @@ backtrack:
     // contradiction: resume the deepest level with untried digits (a donating part: levels
     // below its first live one were given away)
     if (b.depth == (DN ? dd.base : 0u)) {
-        PROF4(3, finish_board4<DN, HI>(w, wr, a, b, c, b.count > 0 ? 1 : 0));
+        PROF4(3, finish_board4<DN, HI, FS>(w, wr, a, b, c, b.count > 0 ? 1 : 0));
         return;
     }
 #if SDK_SOLVE4_PROFILE
@@ -1796,14 +1820,14 @@ backtrack:
 }
 
 // step of slot HI: its state comes from and returns to LDS; returns whether the slot is active
-template <bool DN, int HI, bool SV = false>
+template <bool DN, int HI, bool SV = false, bool FS = false>
 __device__ __forceinline__ bool step4(const Lane4& wr, const Args4& a, Cells4& c, bool bad, uint2 (*s_stk)[2][64],
                                       uint2* g_stk_all, Slot4* s_slot, uint2* s_region, uint8_t* s_in) {
     const Lane4 w = lane4_fresh(s_region, s_in);
     uint2* g_stk = g_stk_all + (size_t)blockIdx.x * (kMaxDepth * 2 * 64);
     Slot4* p = s_slot + w.half * 2 + HI;
     Slot4 b;
-    PROF4(1 + HI, b = *p; step4_body<DN, HI, SV>(w, wr, a, b, c, bad, s_stk, g_stk); if (w.hl == 0) *p = b);
+    PROF4(1 + HI, b = *p; step4_body<DN, HI, SV, FS>(w, wr, a, b, c, bad, s_stk, g_stk); if (w.hl == 0) *p = b);
     return (b.active & 1u) != 0u;
 }
 
@@ -1828,7 +1852,9 @@ __device__ __forceinline__ bool first_board4(const Lane4& w, const Args4& a, Cel
 // VGPRs at 5 waves per SIMD keep its round free of scratch reloads (at 6: 48 B/lane spilled)
 #define SDK_SOLVE4_DN_WAVES_PER_EU 5
 #endif
-template <bool DN, bool SV = false>   // SV: the split phase of a phased solve (split_save4)
+// SV: the split phase of a phased solve (split_save4); FS: a first-solution scan of a lex frontier
+// (boards above the lowest hit are cancelled, see s_found4)
+template <bool DN, bool SV = false, bool FS = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOLVE4_DN_WAVES_PER_EU : SDK_SOLVE4_WAVES_PER_EU))) void solve4_kernel(SolveArgs args) {
     // the donation phases are enqueued without the host: their board count comes from the
     // device (the list the previous phase left), and the launch is the full resident grid, of
@@ -1908,6 +1934,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         a.nseg = min<uint32_t>(kHeads, grid);
         a.seg_size = (a.tail0 + a.nseg - 1) / a.nseg;
         if (SV && threadIdx.x == 0) s_save4 = SaveP4{static_cast<SplitSave*>(args.save), args.save_idx};
+        if (FS && threadIdx.x == 0) s_found4 = args.found;
     }
 
     Cells4 c;
@@ -1951,13 +1978,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         if (E0 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E0))
-                r = step4<DN, 0, SV>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot, s_region, s_in);
+                r = step4<DN, 0, SV, FS>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B0), s_stk, g_stk, s_slot, s_region, s_in);
             A0 = (A0 & ~E0) | (__builtin_amdgcn_ballot_w64(r) & E0);
         }
         if (E1 != 0) {
             bool r = false;
             if (__builtin_amdgcn_inverse_ballot_w64(E1))
-                r = step4<DN, 1, SV>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot, s_region, s_in);
+                r = step4<DN, 1, SV, FS>(w, a, c, __builtin_amdgcn_inverse_ballot_w64(B1), s_stk, g_stk, s_slot, s_region, s_in);
             A1 = (A1 & ~E1) | (__builtin_amdgcn_ballot_w64(r) & E1);
         }
         if (DN && (E0 | E1) != 0) {

@@ -13,6 +13,8 @@ hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream) 
         solve4_kernel<true><<<grid, 64, 0, stream>>>(a);
     else if (a.save)   // the split phase of a phased solve: saves the stacks it stops
         solve4_kernel<false, true><<<grid, 64, 0, stream>>>(a);
+    else if (a.found)  // a first-solution scan of a lex frontier: cancels boards above the lowest hit
+        solve4_kernel<false, false, true><<<grid, 64, 0, stream>>>(a);
     else
         solve4_kernel<false><<<grid, 64, 0, stream>>>(a);
     return hipGetLastError();

@@ -84,7 +84,12 @@ struct SolveArgs {
     void* save = nullptr;      // QUAD split phase: stacks of boards that reach the split budget
                                // (solve4_kernel.h SplitSave; nullable)
     uint32_t* save_idx = nullptr;   // ... and each saved board's entry (by board index)
+    long long* found = nullptr;     // QUAD first-solution scan (sdk_frontier_first): the lowest board
+                                    // index (in_first + i * in_step) with status 1 or -2 so far; boards
+                                    // above it are cancelled (solve4_kernel.h, s_found4)
 };
+// status of a board a first-solution scan stopped because it lies above a lower board's hit
+constexpr int kStCancelled = -3;
 
 // per-XCD dequeue: the first n - n/128 boards are cut into kHeads contiguous segments with a
 // head each, workgroup g takes chunks of segment g % kHeads (the XCD the round-robin

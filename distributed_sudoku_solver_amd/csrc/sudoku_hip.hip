@@ -285,11 +285,14 @@ struct sdk_ctx {
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
     int dn_blocks_per_cu = 0;      // resident solve4_kernel<true> workgroups per CU (queried once)
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
+    DevBuf fr_tail;                // refine_head: the boards kept after the refined ones
     // the device-resident frontier of the last sdk_frontier_build (in fr_a)
     uint64_t fr_size = 0;
     uint64_t fr_leaves = 0;
     uint32_t fr_levels = 0;
     bool fr_valid = false;
+    int fr_mode = SDK_FRONTIER_COUNT;   // kept by refinements and loaded records
+    long long* first_found = nullptr;   // set by frontier_first for its solve launch (SolveArgs::found)
     // RCCL communicator (sdk_comm_init), one rank per context
     ncclComm_t comm = nullptr;
     int comm_rank = 0;
@@ -480,6 +483,8 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     a.n_dev = nullptr;
     a.save = nullptr;
     a.save_idx = nullptr;
+    // a first-solution scan (frontier_first): the plain QUAD launch cancels boards above the lowest hit
+    a.found = (four && !count_mode && dn_phase == 0) ? c->first_found : nullptr;
     if (dn_phase == 1 && c->dn_resume_now && four && !count_mode) {
         // the split phase leaves the stacks of the boards it stops (sdk::split_save4)
         a.save = c->dn_save.p;
@@ -803,6 +808,7 @@ int run_frontier_levels(sdk_ctx* c, uint64_t m0, bool use_mask, int mode, uint64
 
 int build_frontier(sdk_ctx* c, const uint8_t* h_board, const uint16_t* h_mask, int mode, uint64_t target) {
     c->fr_valid = false;
+    c->fr_mode = mode;
     if (target == 0) target = (uint64_t)c->cus * (uint64_t)c->waves_per_cu * 8ull;
     int rc;
     if ((rc = ensure(c->fr_a, frontier_capacity(1, target) * 81)) || (rc = ensure(c->fr_mask, 16))) return rc;
@@ -841,7 +847,43 @@ int refine_frontier(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t end, uin
         c->fr_valid = true;
         return SDK_OK;
     }
-    return run_frontier_levels(c, n, false, SDK_FRONTIER_COUNT, target, false);
+    return run_frontier_levels(c, n, false, c->fr_mode, target, false);
+}
+
+// Boards [lo, mid) of the current frontier refined as refine_frontier does (step 1), followed by
+// boards [mid, hi) unchanged: a first-solution search splits the one board that hit its node
+// budget (mid = lo + 1) without expanding the rest of its live range.  In first mode the result
+// is still sorted by completion (the refined boards' children keep their order and precede
+// board mid's completions).
+int refine_head(sdk_ctx* c, uint64_t lo, uint64_t mid, uint64_t hi, uint64_t target) {
+    if (!c->fr_valid) return fail(SDK_EINVAL, "no frontier: call sdk_frontier_build first");
+    hi = std::min(hi, c->fr_size);
+    lo = std::min(lo, hi);
+    mid = std::min(std::max(mid, lo), hi);
+    const uint64_t tail = hi - mid;
+    int rc;
+    if (tail) {   // the kept boards go aside first: the refinement reuses both frontier buffers
+        if ((rc = ensure(c->fr_tail, tail * 81))) return rc;
+        HIPCALL(hipMemcpyAsync(c->fr_tail.p, static_cast<const char*>(c->fr_a.p) + mid * 81, tail * 81,
+                               hipMemcpyDeviceToDevice, c->stream));
+    }
+    if ((rc = refine_frontier(c, lo, 1, mid, target))) return rc;
+    if (!tail) return SDK_OK;
+    const uint64_t h = c->fr_size;
+    c->fr_valid = false;
+    if (c->fr_a.bytes < (h + tail) * 81) {
+        DevBuf nb;
+        if ((rc = ensure(nb, (h + tail) * 81))) return rc;
+        if (h) HIPCALL(hipMemcpyAsync(nb.p, c->fr_a.p, h * 81, hipMemcpyDeviceToDevice, c->stream));
+        HIPCALL(hipStreamSynchronize(c->stream));
+        HIPCALL(hipFree(c->fr_a.p));
+        c->fr_a = nb;
+    }
+    HIPCALL(hipMemcpyAsync(static_cast<char*>(c->fr_a.p) + h * 81, c->fr_tail.p, tail * 81, hipMemcpyDeviceToDevice,
+                           c->stream));
+    c->fr_size = h + tail;
+    c->fr_valid = true;
+    return SDK_OK;
 }
 
 // Lex-ordered (SDK_FRONTIER_FIRST) breadth-first expansion of n seed boards, each with its own
@@ -852,6 +894,7 @@ int refine_frontier(sdk_ctx* c, uint64_t first, uint64_t step, uint64_t end, uin
 int expand_boards(sdk_ctx* c, const uint8_t* h_in, const uint16_t* h_masks, uint64_t n, uint64_t target,
                   uint8_t* h_out, uint64_t cap, uint64_t* out_n) {
     c->fr_valid = false;
+    c->fr_mode = SDK_FRONTIER_FIRST;
     *out_n = 0;
     if (n == 0) return SDK_OK;
     if (n > kFrontierCap) return fail(SDK_EINVAL, "at most %llu seed boards", (unsigned long long)kFrontierCap);
@@ -901,8 +944,15 @@ int frontier_first(sdk_ctx* c, uint64_t lo, uint64_t hi, long long* d_found, uin
     if ((rc = ensure(c->out, std::max<uint64_t>(n, 1) * 81)) || (rc = ensure(c->status, std::max<uint64_t>(n, 1))))
         return rc;
     if (n) {
+        // boards above the lowest hit are cancelled inside the launch (solve4_kernel<.., FS>):
+        // d_found is its found word until first_hit_kernel writes the answer.  The plain kernel
+        // (no subtree donation: a heavy board is split by the caller, shard.sharded_solve)
+        sdk::first_init_kernel<<<1, 1, 0, c->stream>>>(d_found);
+        HIPCALL(hipGetLastError());
+        c->first_found = d_found;
         rc = launch_solve(c, static_cast<uint8_t*>(c->fr_a.p), nullptr, static_cast<uint8_t*>(c->out.p),
-                          static_cast<int8_t*>(c->status.p), nullptr, n, 0, 0, nullptr, nullptr, lo, 1);
+                          static_cast<int8_t*>(c->status.p), nullptr, n, 0, 0, nullptr, nullptr, lo, 1, -1, -1, 0);
+        c->first_found = nullptr;
         if (rc) return rc;
     }
     sdk::first_hit_kernel<<<1, 256, 0, c->stream>>>(static_cast<int8_t*>(c->status.p),
@@ -1433,6 +1483,18 @@ int sdk_frontier_refine_range(sdk_ctx* c, uint64_t lo, uint64_t hi, uint64_t tar
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCALL(hipSetDevice(c->device));
     int rc = refine_frontier(c, lo, 1, hi, target);
+    if (rc) return rc;
+    if (size) *size = c->fr_size;
+    if (leaves) *leaves = c->fr_leaves;
+    return SDK_OK;
+}
+
+int sdk_frontier_refine_head(sdk_ctx* c, uint64_t lo, uint64_t mid, uint64_t hi, uint64_t target, uint64_t* size,
+                             uint64_t* leaves) {
+    if (!c) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCALL(hipSetDevice(c->device));
+    int rc = refine_head(c, lo, mid, hi, target);
     if (rc) return rc;
     if (size) *size = c->fr_size;
     if (leaves) *leaves = c->fr_leaves;

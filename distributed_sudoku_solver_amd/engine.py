@@ -333,7 +333,7 @@ class SudokuEngine:
 
     def frontier_load(self, d_boards, n, offset=0):
         """The n records at device buffer `d_boards` (+ offset boards) become the current
-        count-mode frontier."""
+        frontier (in the mode of the frontier built last)."""
         ptr = (d_boards.ptr.value if hasattr(d_boards, "ptr") else int(d_boards)) + 81 * int(offset)
         L.check(self.lib.sdk_frontier_load_dev(self.ctx, ctypes.c_void_p(ptr), int(n)), "sdk_frontier_load_dev")
 
@@ -343,6 +343,15 @@ class SudokuEngine:
         leaves = ctypes.c_uint64()
         L.check(self.lib.sdk_frontier_refine_range(self.ctx, int(lo), int(hi), int(target), ctypes.byref(size),
                                                    ctypes.byref(leaves)), "sdk_frontier_refine_range")
+        return size.value, leaves.value
+
+    def frontier_refine_head(self, lo, mid, hi, target):
+        """Frontier boards [lo, mid) refined towards `target`, then [mid, hi) unchanged: (size, leaves)."""
+        size = ctypes.c_uint64()
+        leaves = ctypes.c_uint64()
+        L.check(self.lib.sdk_frontier_refine_head(self.ctx, int(lo), int(mid), int(hi), int(target),
+                                                  ctypes.byref(size), ctypes.byref(leaves)),
+                "sdk_frontier_refine_head")
         return size.value, leaves.value
 
     # ------------------------------------------- one-board multi-GPU searches

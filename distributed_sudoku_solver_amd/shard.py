@@ -21,10 +21,12 @@ and a partial board, DHT_Node.py:491-510, 225-250; utils.py:1-9):
     boards i = rank, rank+world, ... (interleaved for load balance), and the only
     exchange is one RCCL all-reduce of {count, budget hits} in device memory.
   * sharded_solve: first solution in the reference's DFS order.  The frontier is
-    built in lex order; ranks scan it in interleaved chunks, wave by wave, and
-    after each wave an RCCL all-reduce(min) of the lowest hit index is the
-    found/termination flag; the owner of that index broadcasts the board.  Lower
-    chunks always finish before a higher hit is accepted, so the answer is
+    built in lex order and every live board carries a lex key; ranks work on their
+    live ranges in rounds (boards above the lowest hit cancelled inside each
+    launch, heavy boards refined one level deeper), and before every round an
+    RCCL all-gather of the ranks' states carries the found/termination flag (the
+    lowest hit key) and drives the same record-moving rebalance as the counts.
+    Lower keys always finish before a higher hit is accepted, so the answer is
     identical for every world size.
 The collectives go through a `comm` object: RcclComm (device memory, RCCL over
 xGMI, the product path), hostcomm.TcpComm (host arrays over standard-library
@@ -480,48 +482,170 @@ def _add_to_result(engine, res, k):
         res[:2] = vals
 
 
-def sharded_solve(engine, board, rank, world, comm=None, mask=None, waves=8, target=None):
+KEY_SPACE = 1 << 62       # lex keys of a first-solution search (sharded_solve)
+ROUND_BUDGET = 512        # search nodes per frontier board and round of sharded_solve (refined after)
+
+
+def _key_trim(hi, key_lo, key_step, g):
+    """Live boards [., hi) of a rank whose board t has lex key key_lo + t * key_step: those with
+    a key above g (a completion or budget hit already met at key g) cannot hold the answer."""
+    if g >= INT64_MAX or key_step <= 0:
+        return hi
+    return min(hi, max(0, (g - key_lo) // key_step + 1))
+
+
+def sharded_solve(engine, board, rank, world, comm=None, mask=None, target=None, chunk=None, info=None,
+                  ranges=None, round_budget=None):
     """First completion of `board` in the reference's DFS order, split over `world` ranks.
 
     Returns (out uint8[81], status) with solve_sudoku's contract: the lex-first
     completion and 1, or the input and 0 (no completion) / -2 (node budget hit in
-    a subtree that precedes every completion found)."""
+    a subtree that precedes every completion found; only with a context node budget).
+
+    The lex frontier is built on every rank (replicated, no exchange); frontier board t's
+    completions all precede board t+1's.  Every live board carries a lex KEY (board t of a
+    rank's frontier: key_lo + t * key_step; the replicated frontier spans [0, KEY_SPACE)), so
+    boards on different ranks compare in the reference's DFS order.  Each rank starts on a
+    contiguous block (or `ranges`) and works in rounds:
+      * its live boards [lo, min(hi, lo + chunk)) are solved in one launch with a per-board node
+        budget; boards above the lowest hit (completion or budget hit) stop inside the launch
+        (sdk_frontier_first);
+      * a completion at t makes key(t) the rank's best and ends its range (everything after it
+        is lex-greater); a budget hit at t keeps [t, hi) live, and board t is split into its
+        lex-ordered sub-boards at the start of the next round (engine.frontier_refine_head:
+        the rest of the range stays as it is, keys re-spread monotonically over the same key
+        interval) -- the device form of the reference handing a partial board on
+        (DHT_Node.py:491-510), here to the rank itself and, through the rebalance below, to
+        others;
+      * before every round the ranks all-gather (lo, hi, local, key_lo, key_step, best_key, heavy)
+        (RCCL ncclAllGather of 7 x int64 per rank): the minimum best_key is the found flag --
+        every rank drops its boards keyed above it -- and rebalance_plan gives dry ranks the
+        upper half of the largest live range, as board RECORDS (grouped ncclSend/ncclRecv) when
+        either side no longer holds the replicated frontier.  A rank whose remainder is one board
+        (or heavy: it hit the budget) refines it while another is dry, so one heavy subtree does
+        not stay on one GPU.
+    The search ends when no rank holds a board keyed below the minimum; the owner of that key
+    broadcasts its board.  With a context node budget (SDK_OPT_NODE_BUDGET > 0) budget hits are
+    final (status -2) instead of being refined.  `info` (dict) gets rounds, steals, moved
+    records and refinements."""
     if world > 1 and comm is None:
         raise ValueError("world > 1 needs a comm (RcclComm or HostComm)")
     board = np.ascontiguousarray(board, dtype=np.uint8).reshape(81)
-    if target is None and (board > 9).any():
-        # an out-of-domain given makes its units inexact: sub-boards lex-after the answer can take
-        # exponential refutations, and every board of a scanned chunk is solved to its end
-        # (an empty board plus one inert given: 53 s at the default frontier, 0.3 ms unsplit,
-        # tools/frontier_first_probe.py), so such a board is searched unsplit -- the reference's
-        # own DFS order, one slot
-        target = 1
     size, _ = engine.frontier_build(board, mask=mask, mode=L.SDK_FRONTIER_FIRST,
                                     target=default_target(engine, world) if target is None else target)
     if size == 0:
         return board.copy(), 0
-    chunk = max(1, -(-size // (world * waves)))
-    nchunks = -(-size // chunk)
+    user_budget = int(engine.get_option(L.SDK_OPT_NODE_BUDGET) or 0)
+    rbudget = user_budget or int(round_budget or ROUND_BUDGET)
+    if chunk is None:    # the whole live range per round: the launch cancels what lies above a hit
+        chunk = 1 << 62
+    split = 2
+    key_lo, key_step = 0, KEY_SPACE // size
+    lo, hi = shard_bounds(size, rank, world) if ranges is None else (int(ranges[rank][0]), int(ranges[rank][1]))
+    lo, hi = min(lo, size), min(hi, size)
+    local = heavy = 0
+    my_best = INT64_MAX                                   # key of this rank's lowest hit
     found = engine.result_buffer(1, np.int64)
     best = engine.result_buffer(82, np.uint8)
+    keep = engine.result_buffer(82, np.uint8)            # the board behind my_best
+    mine = engine.result_buffer(7, np.int64)
+    allr = engine.result_buffer(7 * world, np.int64)
+    inbox = None
+    rounds = steals = moved = refined = 0
+    g = INT64_MAX
+    owner = rank
+    engine.set_option(L.SDK_OPT_NODE_BUDGET, rbudget)
     try:
-        for wave in range(-(-nchunks // world)):
-            k = wave * world + rank
-            engine.frontier_first(k * chunk, min((k + 1) * chunk, size), found, best)
+        while True:
             if comm is not None:
-                comm.allreduce(found, 1, np.int64, "min")         # found / termination flag
-            g = int(engine.read(found, 1, np.int64)[0])
-            if g != INT64_MAX:
-                if comm is not None:
-                    comm.broadcast(best, 82, (g // chunk) % world)
-                b = engine.read(best, 82, np.uint8)
-                st = int(b[81].view(np.int8))
-                return (b[:81].copy() if st == 1 else board.copy()), st
+                _store(mine, [lo, hi, local, key_lo, key_step, my_best, heavy], np.int64)
+                comm.allgather(mine, allr, 56)
+                S = engine.read(allr, 7 * world, np.int64).reshape(world, 7).tolist()
+            else:
+                S = [[lo, hi, local, key_lo, key_step, my_best, heavy]]
+            g = min(s[5] for s in S)                      # found / termination flag
+            owner = min(range(len(S)), key=lambda k: (S[k][5], k))
+            for s in S:                                   # boards keyed above the lowest hit are done
+                s[1] = _key_trim(s[1], s[3], s[4], g)
+                if s[1] <= s[0]:
+                    s[6] = 0
+            if all(s[1] <= s[0] for s in S):
+                break
+            skip = False
+            if comm is not None:
+                newS, moves, refines = rebalance_plan([s[:3] + [s[6]] for s in S], min_split=split)
+                steals += sum(1 for a, b in zip(S, newS) if a[1] <= a[0] and b[1] > b[0])
+                ops, got = [], None
+                for donor, recv, mid, end, by_records in moves:
+                    if rank == recv:                      # the keys of what this rank takes over
+                        d = S[donor]
+                        key_lo, key_step = (d[3] + mid * d[4], d[4]) if by_records else (d[3], d[4])
+                    if not by_records:
+                        continue
+                    moved += end - mid
+                    if rank == donor:
+                        ops.append((L.SDK_COMM_SEND, recv) + engine.frontier_records(mid, end))
+                    elif rank == recv:
+                        inbox = _grow_records(engine, inbox, end - mid)
+                        ops.append((L.SDK_COMM_RECV, donor, inbox, 81 * (end - mid)))
+                        got = end - mid
+                if any(m[4] for m in moves):
+                    comm.p2p(ops)                         # every rank: a collective on host transports
+                if got is not None:
+                    engine.frontier_load(inbox, got)      # received records: board t has key key_lo + t * step
+                lo, hi, local = (int(v) for v in newS[rank])
+                heavy = S[rank][6]
+                if rank in refines and not user_budget:
+                    heavy, skip = 1, True                 # refine now; the next round can split it
+            else:
+                lo, hi, heavy = S[0][0], S[0][1], S[0][6]
+            if heavy and hi > lo and not user_budget:
+                # the heavy board (the first live one) split into its lex-ordered sub-boards, the
+                # rest of the range kept as it is; the rank's keys are re-spread over its same
+                # interval [key(lo), key(hi)) -- monotone, so the order across ranks holds
+                k0, k1 = key_lo + lo * key_step, key_lo + hi * key_step
+                n, _ = engine.frontier_refine_head(lo, lo + 1, hi, refine_target(world, split))
+                refined += 1
+                if n and (k1 - k0) // n < 1:
+                    raise RuntimeError("sharded_solve: lex keys exhausted (a range refined ~40 times)")
+                lo, hi, local = 0, n, 1
+                key_lo, key_step = k0, ((k1 - k0) // n if n else 1)
+                heavy = 0
+            end = min(hi, lo + chunk)
+            if end > lo and not skip:
+                engine.frontier_first(lo, end, found, best)
+                f = int(engine.read(found, 1, np.int64)[0])
+                if f == INT64_MAX:
+                    lo = end                              # every board refuted
+                else:
+                    b = engine.read(best, 82, np.uint8)
+                    st = int(b[81].view(np.int8))
+                    if st == -2 and not user_budget:
+                        lo, heavy = f, 1                  # boards below f refuted; f and on stay live
+                    else:
+                        k = key_lo + f * key_step
+                        if k < my_best:
+                            my_best = k
+                            _store(keep, b, np.uint8)
+                        lo = hi                           # the rest of the range is lex-greater
+            rounds += 1
+        status = 0
+        out = board.copy()
+        if g != INT64_MAX:
+            if comm is not None:
+                comm.broadcast(keep, 82, owner)           # the owner of the lowest key has its board
+            b = engine.read(keep, 82, np.uint8)
+            status = int(b[81].view(np.int8))
+            if status == 1:
+                out = b[:81].copy()
     finally:
-        for h in (found, best):
+        engine.set_option(L.SDK_OPT_NODE_BUDGET, user_budget)
+        for h in (found, best, keep, mine, allr, inbox):
             if hasattr(h, "free"):
                 h.free()
-    return board.copy(), 0
+    if info is not None:
+        info.update(rounds=rounds, steals=steals, moved_records=moved, refines=refined, frontier=size)
+    return out, status
 
 
 def _store(buf, values, dtype):
@@ -554,8 +678,10 @@ def rebalance_ranges(ranges, min_split=2):
 
 
 def rebalance_plan(states, min_split=2):
-    """One rebalancing step over the all-gathered rank states (lo, hi, local): `local` = the
-    rank's frontier is no longer the replicated one (it received or refined records).
+    """One rebalancing step over the all-gathered rank states (lo, hi, local[, heavy]): `local` =
+    the rank's frontier is no longer the replicated one (it received or refined records);
+    `heavy` (optional) = its first live board is known to be too heavy to finish in a round (a
+    first-solution search: it hit the round's node budget).
 
     Returns (new_states, moves, refines), a pure function of the gathered values (every rank
     computes the same):
@@ -566,10 +692,13 @@ def rebalance_plan(states, min_split=2):
         board records (81 B each) of [mid, hi) and the receiver's frontier becomes them;
         otherwise only the range travels;
       * if a rank is still empty after that, every rank whose remaining boards are too few to
-        split refines them into their second-level children (refines = [rank]): the next step
-        splits those records -- the device form of the reference handing on a partial board
-        mid-search (DHT_Node.py:502-509), here for a subtree too heavy to leave on one GPU."""
-    S = [[int(a), int(b), int(c)] for a, b, c in states]
+        split refines them into their second-level children (refines = [rank]) -- when that
+        remainder is ONE board or the rank is heavy (a few lighter boards it finishes in the
+        round anyway): the next step splits those records -- the device form of the reference
+        handing on a partial board mid-search (DHT_Node.py:502-509), here for a subtree too heavy
+        to leave on one GPU."""
+    S = [[int(x[0]), int(x[1]), int(x[2])] for x in states]
+    heavy = [bool(x[3]) if len(x) > 3 else False for x in states]
     moves, takers = [], set()
     split = max(2, min_split)
     for r in range(len(S)):
@@ -591,7 +720,8 @@ def rebalance_plan(states, min_split=2):
         takers.add(r)
     refines = []
     if any(b <= a for a, b, _ in S):
-        refines = [k for k in range(len(S)) if 0 < S[k][1] - S[k][0] < split and k not in takers]
+        refines = [k for k in range(len(S)) if 0 < S[k][1] - S[k][0] < split and k not in takers
+                   and (S[k][1] - S[k][0] == 1 or heavy[k])]
     return S, moves, refines
 
 
@@ -680,7 +810,7 @@ def sharded_count_rebalanced(engine, board, rank, world, limit=0, comm=None, tar
                 count += c
                 hits += h
                 lo = end
-                if limit and count >= limit:
+                if limit and count + own_leaves >= limit:
                     lo = hi                                    # this rank alone reached the limit
             rounds += 1
             if comm is None and lo >= hi:                     # single rank, nothing to exchange

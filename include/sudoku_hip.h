@@ -259,7 +259,11 @@ int sdk_frontier_count_dev(sdk_ctx *ctx, uint64_t first, uint64_t step, uint64_t
 /* First mode: solve frontier boards [lo, hi) (each to its lex-first completion)
  * and write the lowest index whose status is not SDK_UNSOLVABLE to d_found
  * (device int64; INT64_MAX if none) and that board's output + status to d_best
- * (device, 82 bytes: board[81], int8 status). */
+ * (device, 82 bytes: board[81], int8 status).  d_found is also the launch's found
+ * word: a board that ends solved or at the node budget lowers it, and boards above
+ * it stop at their next check ("shards whose index is above the
+ * minimum may stop"), so the launch ends once every board below the lowest hit is
+ * decided.  The result is the one a launch that solves every board would give. */
 int sdk_frontier_first_dev(sdk_ctx *ctx, uint64_t lo, uint64_t hi, void *d_found, void *d_best);
 
 /* Frontier records, for moving live subtrees between ranks (SURVEY §8(e) rebalance; the
@@ -268,16 +272,24 @@ int sdk_frontier_first_dev(sdk_ctx *ctx, uint64_t lo, uint64_t hi, void *d_found
  *                             uint8[*size][81] records (valid until the next frontier call
  *                             on this context); send a range of it with sdk_comm_send_dev.
  *   sdk_frontier_load_dev     the n records at d_boards (device, e.g. received with
- *                             sdk_comm_recv_dev) become the current count-mode frontier
- *                             (copied; 0 leaves).
+ *                             sdk_comm_recv_dev) become the current frontier, in the mode
+ *                             of the frontier built last (copied; 0 leaves).
  *   sdk_frontier_refine_range keep frontier boards [lo, hi) and expand them on this device
  *                             until they number `target` (or nothing branches): a rank splits
- *                             its last heavy subtree into second-level records.  *leaves =
- *                             completions met while refining. */
+ *                             its last heavy subtree into second-level records.  The mode is
+ *                             the frontier's: count mode counts the completions met while
+ *                             refining in *leaves; first mode keeps them in place (lex order,
+ *                             *leaves = 0), so the refined range is still sorted by completion. */
 int sdk_frontier_boards_dev(sdk_ctx *ctx, void **d_boards, uint64_t *size);
 int sdk_frontier_load_dev(sdk_ctx *ctx, const void *d_boards, uint64_t n);
 int sdk_frontier_refine_range(sdk_ctx *ctx, uint64_t lo, uint64_t hi, uint64_t target, uint64_t *size,
                               uint64_t *leaves);
+/* Keep boards [lo, mid) refined as sdk_frontier_refine_range does, followed by boards
+ * [mid, hi) unchanged (the new frontier: refined([lo, mid)) ++ [mid, hi)).  A first-solution
+ * search splits the one board that hit its node budget (mid = lo + 1) and keeps the rest of
+ * its live range as it is; in first mode the frontier stays sorted by completion. */
+int sdk_frontier_refine_head(sdk_ctx *ctx, uint64_t lo, uint64_t mid, uint64_t hi, uint64_t target,
+                             uint64_t *size, uint64_t *leaves);
 
 /* RCCL communicator bound to a context (one rank per GPU).  Rank 0 makes the
  * id, the caller distributes it (e.g. over torch.distributed/gloo), every rank

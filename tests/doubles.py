@@ -62,6 +62,7 @@ class OracleEngine:
         from oracle import oracle as O
         self.O = O
         self.calls = []
+        self.opts = {}
 
     def solve_batch(self, boards, masks=None, want_work=False, budget=None, donate=None):
         self.calls.append(len(boards))
@@ -79,7 +80,12 @@ class OracleEngine:
 
     # ---- frontier primitives, restated on the CPU (test double of libsudoku_hip's) ----
     def get_option(self, key):
-        return {L.SDK_OPT_DEVICE_CUS: 1, L.SDK_OPT_WAVES_PER_CU: 2}[key]
+        if key in self.opts:
+            return self.opts[key]
+        return {L.SDK_OPT_DEVICE_CUS: 1, L.SDK_OPT_WAVES_PER_CU: 2, L.SDK_OPT_NODE_BUDGET: 0}[key]
+
+    def set_option(self, key, value):
+        self.opts[key] = int(value)
 
     def frontier_build(self, board, mask=None, mode=L.SDK_FRONTIER_COUNT, target=0):
         """Naive-DFS order expansion (lowest empty cell, digits ascending, utils.py:14-56)
@@ -97,6 +103,13 @@ class OracleEngine:
         """Boards [lo, hi) of the frontier, expanded on until >= target (no leaves dropped here)."""
         self.calls.append(("refine_range", lo, hi, len(self.frontier)))
         self.frontier = self._expand(list(self.frontier[lo:hi]), target, None)
+        return len(self.frontier), 0
+
+    def frontier_refine_head(self, lo, mid, hi, target):
+        """Boards [lo, mid) expanded on until >= target, then [mid, hi) as they are."""
+        self.calls.append(("refine_head", lo, mid, hi, len(self.frontier)))
+        rest = list(self.frontier[mid:hi])
+        self.frontier = self._expand(list(self.frontier[lo:mid]), target, None) + rest
         return len(self.frontier), 0
 
     def frontier_records(self, lo, hi):
@@ -152,11 +165,15 @@ class OracleEngine:
         res[1] = 0
 
     def frontier_first(self, lo, hi, found, best):
+        """The lowest board of [lo, hi) whose naive DFS ends solved or at the node budget
+        (SDK_OPT_NODE_BUDGET, in search nodes: VALIDATIONS_PER_NODE validations each)."""
         hi = min(hi, len(self.frontier))
         self.calls.append(("first", lo, hi))
         found[0] = (1 << 63) - 1
         if hi > lo:
-            out, st, _ = self.O.naive_solve_batch(np.stack(self.frontier[lo:hi]), budget=50_000_000, threads=2)
+            nb = self.get_option(L.SDK_OPT_NODE_BUDGET)
+            out, st, _ = self.O.naive_solve_batch(np.stack(self.frontier[lo:hi]),
+                                                  budget=validation_budget(nb or None, 50_000_000), threads=2)
             hits = np.flatnonzero(st != 0)
             if len(hits):
                 i = int(hits[0])
@@ -272,3 +289,56 @@ class BenchStubEngine(OracleEngine):
 
     def close(self):
         pass
+
+
+class StagedDeviceComm:
+    """shard.RcclComm's interface over a host transport (hostcomm.TcpComm) for REAL engines on
+    one GPU (test only): device buffers and record addresses are staged through host memory.
+    RCCL refuses two ranks on one device, so a 1-GPU box runs the multi-rank frontier searches
+    (record moves, refinements, the all-gathered found flag) over two contexts this way; only
+    the RCCL transport itself is left to the driver's multi-GPU node."""
+
+    def __init__(self, engine, tcp):
+        self.engine, self.tcp = engine, tcp
+        self.rank, self.world = tcp.rank, tcp.world
+
+    def _down(self, buf, nbytes):
+        import ctypes
+        host = np.empty(int(nbytes), np.uint8)
+        if nbytes:
+            src = buf.ptr if hasattr(buf, "ptr") else ctypes.c_void_p(int(buf))
+            L.check(self.engine.lib.sdk_memcpy_d2h(self.engine.ctx, ctypes.c_void_p(host.ctypes.data), src,
+                                                   host.nbytes), "d2h")
+        return host
+
+    def allreduce(self, buf, count, dtype, op):
+        host = self._down(buf, count * np.dtype(dtype).itemsize).view(dtype)
+        self.tcp.allreduce(host, count, dtype, op)
+        buf.upload(host)
+
+    def broadcast(self, buf, nbytes, root):
+        host = self._down(buf, nbytes)
+        self.tcp.broadcast(host, nbytes, root)
+        buf.upload(host)
+
+    def allgather(self, send, recv, nbytes):
+        host = self._down(send, nbytes)
+        out = np.empty(self.world * nbytes, np.uint8)
+        self.tcp.allgather(host, out, nbytes)
+        recv.upload(out)
+
+    def p2p(self, ops):
+        staged, recvs = [], []
+        for kind, peer, buf, nbytes in ops:
+            if kind == L.SDK_COMM_SEND:
+                staged.append((kind, peer, self._down(buf, nbytes), nbytes))
+            else:
+                host = np.empty(int(nbytes), np.uint8)
+                staged.append((kind, peer, host, nbytes))
+                recvs.append((buf, host))
+        self.tcp.p2p(staged)
+        for buf, host in recvs:
+            buf.upload(host)
+
+    def close(self):
+        self.tcp.close()

@@ -230,13 +230,12 @@ DEMO = "000100000000320000000009000000000070000000000000900000000000900000000003
 @pytest.mark.parametrize("target", [1, 50, 0, None])
 def test_frontier_first_solution_matches_reference(engine, solve_cases, target):
     """sharded_solve (lex-ordered frontier scan) reproduces every golden solve case,
-    including TASK ranges and unsolvable boards, at several frontier sizes (one test per size:
-    ~20 s each on one MI355X, far inside the per-test limit)."""
+    including TASK ranges, unsolvable boards and boards with out-of-domain givens, at several
+    frontier sizes (the full default frontier included: boards above the lowest hit are
+    cancelled inside the launch)."""
     from distributed_sudoku_solver_amd.shard import sharded_solve
     for c in solve_cases[:40]:
         board = np.array(c["puzzle"], np.uint8)
-        if target == 0 and (board > 9).any():
-            continue   # forced full frontier on an inexact board: tools/frontier_first_probe.py (53 s)
         out, st = sharded_solve(engine, board, 0, 1, mask=O.range_mask(*c["range"]), target=target)
         assert (st == 1) == c["ok"], (c["name"], target)
         assert out.tolist() == (c["board"] if c["ok"] else c["puzzle"]), (c["name"], target)
@@ -249,8 +248,113 @@ def test_frontier_first_solution_random_vs_oracle(engine):
     for i, b in enumerate(puz):
         if ref_st[i] == -2:
             continue
-        out, st = sharded_solve(engine, b, 0, 1, waves=3)
+        out, st = sharded_solve(engine, b, 0, 1, chunk=4096)
         assert st == ref_st[i] and (out == ref_out[i]).all(), i
+
+
+def test_frontier_first_inexact_board_default_frontier(engine, solve_cases):
+    """a board with an out-of-domain given (its units inexact) searched over
+    the full default lex frontier.  Without in-launch cancellation every sub-board lex-after the
+    answer was refuted to its end (an empty board plus one inert given: 53 s, round 4); now the
+    boards above the lowest hit stop at their next check.  Answer = the reference's."""
+    import time
+    from distributed_sudoku_solver_amd.shard import sharded_solve
+    inexact = [c for c in solve_cases if (np.array(c["puzzle"]) > 9).any()]
+    assert inexact
+    worst = 0.0
+    for c in inexact:
+        board = np.array(c["puzzle"], np.uint8)
+        sharded_solve(engine, board, 0, 1, mask=O.range_mask(*c["range"]), target=0)   # warm
+        t0 = time.perf_counter()
+        out, st = sharded_solve(engine, board, 0, 1, mask=O.range_mask(*c["range"]), target=0)
+        worst = max(worst, time.perf_counter() - t0)
+        assert (st == 1) == c["ok"] and out.tolist() == (c["board"] if c["ok"] else c["puzzle"]), c["name"]
+    print(f"inexact boards: {len(inexact)}, slowest first-solution search {1e3 * worst:.2f} ms")
+    assert worst < 0.5, worst
+
+
+def _two_contexts(fn):
+    """fn(engine, rank, world, comm) on two contexts of GPU 0 in two threads, the comm staged
+    through a TcpComm (RCCL refuses two ranks on one device); returns both results."""
+    import socket
+    import threading
+    from distributed_sudoku_solver_amd.engine import SudokuEngine
+    from distributed_sudoku_solver_amd.hostcomm import TcpComm
+    from doubles import StagedDeviceComm
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    res, errs = [None, None], []
+
+    def run(r):
+        eng = SudokuEngine(0)
+        comm = None
+        try:
+            comm = StagedDeviceComm(eng, TcpComm(r, 2, "127.0.0.1", port, timeout=60))
+            res[r] = fn(eng, r, 2, comm)
+        except BaseException as e:   # re-raised below
+            errs.append(e)
+        finally:
+            if comm is not None:
+                comm.close()
+            eng.close()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    if errs:
+        raise errs[0]
+    return res
+
+
+def test_two_rank_count_moves_device_records():
+    """the record-moving rebalance on real frontiers -- rank 0 holds ONE heavy board
+    (the 16-clue C5 board as a one-board frontier), rank 1 nothing: rank 0 refines it on the GPU
+    (sdk_frontier_refine_range), sends half of the records from its device frontier
+    (sdk_frontier_boards_dev), rank 1 installs them (sdk_frontier_load_dev) and counts; the total
+    is exact on both ranks."""
+    from distributed_sudoku_solver_amd.shard import sharded_count_rebalanced
+    b16 = synth.parse(synth.SEEDS17["S1"][:-9] + "000800000")
+
+    def fn(eng, r, w, comm):
+        info = {}
+        total, st, _ = sharded_count_rebalanced(eng, b16, r, w, comm=comm, chunk=64, target=1, info=info,
+                                                ranges=[(0, 1), (1, 1)])
+        return total, st, info
+
+    (t0, s0, i0), (t1, s1, i1) = _two_contexts(fn)
+    assert (t0, s0) == (7309, 1) and (t1, s1) == (7309, 1), (t0, t1)
+    assert i0["refines"] >= 1 and i0["moved_records"] > 0, i0
+    assert i1["moved_records"] == i0["moved_records"]
+
+
+def test_two_rank_first_solution_moves_device_records():
+    """VERDICT r4 item 2 on the GPU: sharded_solve with rank 0 holding one board, rank 1 nothing
+    -- rank 0 splits it (sdk_frontier_refine_head, first mode), moves the upper half of the
+    sub-boards to rank 1, both scan with in-launch cancellation; the reference's answer on both
+    ranks.  Then a hard 17-clue board under a small round budget: budget hits are split again and
+    handed on."""
+    from distributed_sudoku_solver_amd.shard import sharded_solve
+    golden = "234156789179328456568479132391245678425687391687913245752831964816794523943562817"
+
+    def fn(eng, r, w, comm):
+        info = {}
+        out, st = sharded_solve(eng, synth.parse(DEMO), r, w, comm=comm, target=1, ranges=[(0, 1), (1, 1)],
+                                info=info)
+        info2 = {}
+        out2, st2 = sharded_solve(eng, hp[0], r, w, comm=comm, target=1, ranges=[(0, 1), (1, 1)], round_budget=2,
+                                  info=info2)
+        return "".join(map(str, out)), st, info, out2, st2, info2
+
+    hp, hs = synth.make_hard_heaviest(1)      # the committed hard set's heaviest board (hundreds of nodes)
+    a, b = _two_contexts(fn)
+    for o, st, info, o2, st2, info2 in (a, b):
+        assert o == golden and st == 1, (o, st)
+        assert (o2 == hs[0]).all() and st2 == 1, st2
+    assert a[2]["refines"] >= 1 and a[2]["moved_records"] > 0 and b[2]["moved_records"] > 0, (a[2], b[2])
+    assert a[5]["refines"] + b[5]["refines"] >= 1, (a[5], b[5])
 
 
 def test_frontier_count_interleaved_ranks_partition(engine):

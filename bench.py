@@ -39,9 +39,11 @@ METRIC = "puzzles solved/sec (whole node, 17-clue hard) at 1/2/4/8 GPUs; checker
 HBM_PEAK_GBPS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 SOLVE_BYTES_PER_PUZZLE = 163      # 81 in + 81 out + 1 status
 CHECK_BYTES_PER_BOARD = 82        # 81 in + 1 verdict
-# VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction per 2 cycles per SIMD
-# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles (32 lanes/cycle x 2)")
-VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4   # one wave64 VALU per SIMD quad-cycle
+# VALU issue peak: 256 CUs x 4 SIMD-32, one wave64 VALU instruction per 2 cycles per SIMD = 2 per
+# SIMD quad-cycle (MI355X_MICROARCH.md:54: "issues each VALU instruction over 2 cycles (32 lanes/cycle
+# x 2)"); at 2.4 GHz 1.23e12 wave-instr/s.  Round 4 priced it at one per quad-cycle.
+VALU_PER_SIMD_QUAD = 2.0
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4 * VALU_PER_SIMD_QUAD
 # --solver: (SDK_OPT_SOLVER value, kernel name, grid option) -- resolved after the library loads
 SOLVERS = {
     "halfwave": (1, "sdk::solve2_kernel", 8),
@@ -55,9 +57,12 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--pipeline", type=int, default=3,
-                    help="C4: also time the passes alternating over this many engine contexts (batches in "
-                         "flight; 0/1 = skip), reported as `pipelined`")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="C4 headline: passes in flight per rank -- consecutive passes issued on this many engine "
+                         "contexts in turn (own HIP stream, dequeue state and output buffer each), so one pass's "
+                         "launch drain overlaps the next pass's start, as a serving node keeps batches in flight; "
+                         "1 = one context.  The single-context figure and its per-launch kernel time (the "
+                         "roofline's) are reported beside it as `single_stream`")
     ap.add_argument("--workload", choices=["solve17", "solve30"], default="solve17")
     ap.add_argument("--batch", type=int, default=10_000_000, help="C4 puzzles, whole job (sharded over the GPUs)")
     ap.add_argument("--weak-leg", type=int, default=1, help="N > 1: also time --batch puzzles per GPU (weak scaling)")
@@ -95,9 +100,12 @@ def parse_args():
                     help="per-lane reference-DFS leg on a C2 prefix (rank 0, N=1; 0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
                     help="watchdog for the side legs: print what was measured and exit")
-    ap.add_argument("--pmc-pipe", default=os.path.join(ROOT, "profiles", "r04", "pmc_pipe.json"),
+    ap.add_argument("--pmc-pipe", default=os.path.join(ROOT, "profiles", "r05", "pmc_pipe.json"),
                     help="per-SIMD pipe counters of the solve kernel (tools/pmc_r04.sh; '' = none)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r03", "pmc_c4.json"),
+    ap.add_argument("--issue-calib", default=os.path.join(ROOT, "profiles", "r05", "issue_calib_pmc.json"),
+                    help="VALU issue ceilings of the solve kernel's instruction mix (tools/issue_calib.hip under "
+                         "rocprofv3, tools/issue_calib_summary.py; '' = none)")
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r05", "pmc_c4.json"),
                     help="per-launch PMC figures of the C4 solve kernel and the C3 checker from rocprofv3 passes "
                          "of this bench at its default sizes (tools/pmc_c4.sh); '' = report traffic null")
     ap.add_argument("--engine-factory", default="", help=argparse.SUPPRESS)
@@ -148,10 +156,31 @@ def pmc_record(path, kernel, units):
     if not path or not os.path.exists(path):
         return None
     with open(path) as f:
-        rec = json.load(f).get(kernel)
+        recs = json.load(f)
+    # a kernel's record is keyed by its full name (template arguments included: the plain
+    # sdk::solve4_kernel<false, false, false>) or by the bare name
+    rec = recs.get(kernel) or next((v for k, v in recs.items() if k.startswith(kernel + "<")
+                                    and k.endswith("<false, false, false>")), None)
     if rec is None or int(rec.get("units_per_launch", -1)) != int(units):
         return None
     return rec
+
+
+def mix_ceiling(path):
+    """VALU issue ceiling of the solve kernel's own instruction mix (tools/issue_calib.hip k_mix: the
+    exact-wave round's VALU -- unit4x and three upd4x, 3-source VOP3 and packed VOP3P ops -- on
+    registers, every SIMD full), VALU wave-instructions per SIMD quad-cycle, or None."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        recs = json.load(f)
+    out = {}
+    for key in ("k_mix@8", "k_round<true>@8", "k_int2@8", "k_or3@8", "k_pk@8"):
+        r = recs.get(key, {}).get("pipe")
+        if r and r.get("valu_per_quad") is not None:
+            out[key] = {"valu_per_quad": r["valu_per_quad"], "dual_frac": r.get("valu_dual_frac"),
+                        "waves_per_simd": r.get("waves_per_simd")}
+    return out or None
 
 
 def pipe_record(path, run, units):
@@ -807,7 +836,20 @@ def main():
     gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
     puzzles, expected = gen(hi - lo, seed=args.seed, lo=lo)
     n = hi - lo
-    elapsed_max, avg_kernel_s, bad_total = solve_leg(eng, d, args, puzzles, expected, args.steps, args.warmup)
+    # one context first: its per-launch HIP events are the kernel's own duration (the roofline's
+    # denominator); then the headline with `inflight` passes in flight (every pass solves the whole
+    # slice, every output buffer is checked)
+    s_el, avg_kernel_s, bad_total = solve_leg(eng, d, args, puzzles, expected, args.steps, args.warmup)
+    single_stream = {"value": total * args.steps / s_el, "unit": "puzzles/s", "ms_per_step": s_el / args.steps * 1e3,
+                     "avg_kernel_ms": avg_kernel_s * 1e3, "contexts": 1,
+                     "parity": {"mismatched_boards": bad_total, "checked_boards": total}}
+    inflight = max(1, args.inflight)
+    if inflight > 1:
+        elapsed_max, _, bad_if = solve_leg(eng, d, args, puzzles, expected, args.steps, args.warmup,
+                                           contexts=inflight, timed=False)
+        bad_total += bad_if
+    else:
+        elapsed_max = s_el
 
     value = total * args.steps / elapsed_max
     achieved = SOLVE_BYTES_PER_PUZZLE * n / avg_kernel_s / 1e9
@@ -826,23 +868,38 @@ def main():
         "traffic_raw": srec.get("traffic_raw") if srec else None,
         "kernel": solve_kernel,
         "avg_kernel_ms": avg_kernel_s * 1000.0,
-        "note": "the search is VALU-issue bound (roofline.valu: SIMD quad-cycles with VALU issue); HBM "
-                "fraction reported per contract (163 algorithmic B per puzzle)",
+        "note": "the search is bound by VALU issue (roofline.valu: against the 2-per-quad-cycle peak and the "
+                "ceiling of the kernel's own instruction mix); HBM fraction reported per contract (163 "
+                "algorithmic B per puzzle)",
     }
     prec = pipe_record(args.pmc_pipe, "c4", n) if args.workload == "solve17" else None
     if prec and prec.get("valu_insts") and prec.get("clock_ghz"):
-        # per SIMD, from a PMC pass of this exact launch (tools/pmc_r04.sh, tools/pmc_pipe_summary.py):
-        # a wave64 VALU instruction holds its SIMD's VALU issue for one quad-cycle, and a SIMD
-        # issues two in some quad-cycles (SQ_ACTIVE_INST_VALU2); the roofline fraction is the share
-        # of SIMD quad-cycles that issued VALU at all
-        single = 256 * 4 * prec["clock_ghz"] * 1e9 / 4
+        # per SIMD, from a PMC pass of this exact launch (tools/pmc_r04.sh, tools/pmc_pipe_summary.py),
+        # priced at the issue peak of 2 wave64 VALU per SIMD quad-cycle at the profiled clock; beside
+        # it the ceiling this kernel's own instruction mix reaches on this GPU (tools/issue_calib.hip:
+        # its 3-source VOP3 and packed VOP3P ops do not dual-issue, so the mix tops out near one per
+        # quad-cycle with every SIMD full)
+        quads_per_s = 256 * 4 * prec["clock_ghz"] * 1e9 / 4
+        peak = quads_per_s * VALU_PER_SIMD_QUAD
         rate = prec["valu_insts"] / avg_kernel_s
+        mix = mix_ceiling(args.issue_calib)
+        mix_q = (mix or {}).get("k_mix@8", {}).get("valu_per_quad")
         roofline["valu"] = {
-            "bound": "valu-issue", "achieved": rate, "unit": "wave-instr/s", "peak": single,
-            "peak_note": "one wave64 VALU issue per SIMD quad-cycle at the profiled clock; dual issue in "
-                         "valu_dual_frac of the quad-cycles lets achieved exceed it",
-            "frac": prec["valu_busy_frac"],
-            "frac_note": "SIMD quad-cycles with VALU issue: (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / quad-cycles",
+            "bound": "valu-issue", "achieved": rate, "unit": "wave-instr/s", "peak": peak,
+            "peak_note": "2 wave64 VALU per SIMD quad-cycle (one per 2 cycles on a SIMD-32, MI355X_MICROARCH.md:54) "
+                         "x 1024 SIMDs at the profiled clock",
+            "frac": rate / peak,
+            "valu_per_quad": rate / quads_per_s,
+            "mix_ceiling": ({"valu_per_quad": mix_q, "wave_instr_per_s": mix_q * quads_per_s,
+                             "frac": rate / (mix_q * quads_per_s),
+                             "note": "tools/issue_calib.hip k_mix at 8 waves/SIMD: the exact round's VALU "
+                                     "(unit4x + 3 upd4x) on registers; VOP3 3-source and VOP3P packed ops "
+                                     "dual-issue in ~7 % of quad-cycles (2-operand VOP2 ops: 78 %)",
+                             "calibration": mix, "source": os.path.relpath(args.issue_calib, ROOT)}
+                            if mix_q else None),
+            "issue_busy_frac": prec["valu_busy_frac"],
+            "issue_busy_note": "SIMD quad-cycles with any VALU issue: (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / "
+                               "quad-cycles; dual issue in valu_dual_frac of them",
             "valu_insts_per_puzzle": prec["valu_insts"] / n,
             "lds_insts_per_puzzle": (prec.get("lds_insts") or 0) / n,
             "salu_insts_per_puzzle": (prec.get("salu_insts") or 0) / n,
@@ -851,7 +908,7 @@ def main():
         }
     elif srec and srec.get("valu_insts"):
         # older PMC record (no per-SIMD counters): VALU wave-instructions per launch over the issue
-        # rate of one per SIMD quad-cycle at 2.4 GHz
+        # peak of 2 per SIMD quad-cycle at 2.4 GHz
         peak = VALU_PEAK_WAVE_INSTR_PER_S
         rate = srec["valu_insts"] / avg_kernel_s
         roofline["valu"] = {
@@ -884,9 +941,11 @@ def main():
             "order": args.order,
             "solver": args.solver,
             "parallelism": f"batch-shard x{d.world} (contiguous slices, no collectives)",
+            "passes_in_flight_per_gpu": inflight,
         },
+        "single_stream": single_stream,
         "roofline": roofline,
-        "parity": {"mismatched_boards": bad_total, "checked_boards": total},
+        "parity": {"mismatched_boards": bad_total, "checked_boards": total * (1 + inflight if inflight > 1 else 1)},
     }
 
     # side legs run under a watchdog: if one stalls (e.g. a collective), rank 0
@@ -912,24 +971,10 @@ def main():
             result[name] = {"error": f"{type(e).__name__}: {e}"}
         return result[name]
 
-    # ------------------------------------------------ batches in flight
-    if args.pipeline > 1:
-        def _pipelined():
-            steps = max(args.steps, 3 * args.pipeline)
-            p_el, _, p_bad = solve_leg(eng, d, args, puzzles, expected, steps, args.warmup, contexts=args.pipeline,
-                                       timed=False)
-            return {"contexts": args.pipeline, "steps": steps, "value": total * steps / p_el, "unit": "puzzles/s",
-                    "ms_per_step": p_el / steps * 1000.0, "vs_single_stream": (total * steps / p_el) / value,
-                    "parity": {"mismatched_boards": p_bad, "checked_boards": total * args.pipeline},
-                    "note": "the same passes issued on that many engine contexts in turn (own HIP stream, "
-                            "dequeue state and output buffer each): one pass's launch drain overlaps the "
-                            "next pass's start; `value` above is one context"}
-        side("pipelined", _pipelined)
-
     # ------------------------------------------------ weak-scaling figure
     if d.world > 1 and args.weak_leg:
         wp, we = gen(total, seed=args.seed, lo=d.rank * total)
-        w_el, w_k, w_bad = solve_leg(eng, d, args, wp, we, args.steps, 1)
+        w_el, w_k, w_bad = solve_leg(eng, d, args, wp, we, args.steps, 1, contexts=inflight, timed=inflight == 1)
         del wp, we
         result["weak_scaling"] = {
             "workload": f"C4 with {total} puzzles PER GPU (rows [rank*{total}, (rank+1)*{total}) of the same stream)",

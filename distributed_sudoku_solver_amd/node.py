@@ -187,6 +187,7 @@ class SudokuNode:
         self.tasks = queue.Queue()               # pending TASK dicts
         self.neighbor_tasks = []                 # tasks handed to the neighbour (re-run on its failure)
         self.hard = []                           # _HardTask: budget-hit tasks (the search thread's round robin)
+        self._leaving = False                    # graceful stop(): tasks still in hand go to the neighbour
         self.busy = False                        # the worker runs a batch
         self.searching = False                   # the search thread runs a slice
         self.done_uuids = _RecentSet()           # uuids already solved somewhere in the ring
@@ -252,6 +253,9 @@ class SudokuNode:
         (DHT_Node.py:137-156); graceful=False simulates a crash."""
         if graceful and self.running:
             with self.lock:
+                # from here on a task the worker or the search thread still holds (a slice or a
+                # batch in flight) is handed on when it comes back (_keep_hard), not re-queued
+                self._leaving = True
                 pending = self._drain_queue() + [h.task for h in self.hard]
                 self.hard = []
                 if self.neighbor and self.neighbor != self.me:
@@ -604,11 +608,10 @@ class SudokuNode:
                 s = LexSearch.for_node(self.search_engine, b, int(m), budget=self.node_budget,
                                        width=self.search_width, max_pending=self.search_max_pending,
                                        slice_target_s=self.slice_target_s)
-                with self.lock:
-                    self.hard.append(_HardTask(t, s, time.monotonic() + self.search_limit_s))
-                with self._work:
-                    self._work.notify_all()
-                self._log("budget hit, continuing", t.get("uuid"))
+                if self._keep_hard(_HardTask(t, s, time.monotonic() + self.search_limit_s)):
+                    with self._work:
+                        self._work.notify_all()
+                    self._log("budget hit, continuing", t.get("uuid"))
             else:
                 self._task_done(t, int(st), o)
 
@@ -626,9 +629,22 @@ class SudokuNode:
         if done:
             self._task_done(h.task, int(h.search.status), h.search.board)
         else:
-            with self.lock:
-                if h.task.get("uuid") not in self.done_uuids:
-                    self.hard.append(h)
+            self._keep_hard(h)
+
+    def _keep_hard(self, h):
+        """Queue a budget-hit task for the search thread -- or, once a graceful stop() has drained
+        the queues, hand it to the neighbour like the rest (the task of a slice in flight
+        used to come back after the drain and wait out its POST).  Returns whether it was queued."""
+        with self.lock:
+            if h.task.get("uuid") in self.done_uuids:
+                return False
+            if not self._leaving:
+                self.hard.append(h)
+                return True
+            nb = self.neighbor if self.neighbor and self.neighbor != self.me else None
+        if nb:
+            self.send(h.task, nb)
+        return False
 
     def _task_done(self, t, st, o):
         """Report a finished task: its completion, 'no completion in this range' (NO_SOLUTION) or

@@ -695,3 +695,26 @@ def test_multi_device_expand_is_an_ordered_partition():
     ref_out, ref_st, _ = O.naive_solve_batch(one, budget=10_000_000, threads=2)
     ref = ["".join(map(str, o)) for o, s_ in zip(ref_out, ref_st) if s_ == 1]
     assert sols[0] == DEMO8_FIRST and sorted(set(sols)) == sorted(set(ref))
+
+
+def test_task_in_flight_at_graceful_stop_goes_to_neighbour():
+    """a budget-hit task whose search slice (or batch launch) is in flight when a graceful
+    stop() drains the queues comes back after the drain; it must go to the neighbour like the rest
+    instead of waiting in a queue nobody serves."""
+    from distributed_sudoku_solver_amd import node as N
+    node = SudokuNode("127.0.0.1", 0, 0, engine=OracleEngine(), delay_ms=0)
+    try:
+        sent = []
+        node.send = lambda msg, to: sent.append((msg, to))
+        task = {"method": "TASK", "sudoku": _grid(synth.WIKI), "uuid": "u1"}
+        h = N._HardTask(task, None, time.monotonic() + 10)
+        assert node._keep_hard(h) and node.hard == [h]               # running: queued for the search thread
+        node.hard = []
+        node.neighbor = ("127.0.0.1", 1)
+        with node.lock:
+            node._leaving = True                                    # what stop(graceful=True) sets
+        assert not node._keep_hard(h) and node.hard == []
+        assert sent == [(task, ("127.0.0.1", 1))]
+    finally:
+        node.httpd.server_close()
+        node.sock.close()

@@ -30,10 +30,10 @@ for s in $steps; do
       || { echo "rocprof failed"; tail -20 "$out/prof.err"; exit 1; }
     find "$out/prof" -name '*kernel_stats.csv' -exec cat {} \; ;;
   prof_c4)   # the headline launch alone: solve4_kernel's average = the C4 launch the bench line times
-             # (single stream: --pipeline 0 leaves out the overlapped passes of the `pipelined` figure)
+             # (single stream: --inflight 1, one context, per-launch HIP events)
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$root/$out/prof_c4" -o run \
       --output-format csv -- python3 "$root/bench.py" --check-boards 0 --c2-puzzles 0 --minimal-puzzles 0 --hard-leg 0 \
-      --count-leg 0 --lane-puzzles 0 --cpu-seconds 0 --http-requests 0 --pipeline 0 > "$root/$out/prof_c4_bench.json" 2> "$root/$out/prof_c4.err") \
+      --count-leg 0 --lane-puzzles 0 --cpu-seconds 0 --http-requests 0 --inflight 1 > "$root/$out/prof_c4_bench.json" 2> "$root/$out/prof_c4.err") \
       || { echo "rocprof c4 failed"; tail -20 "$out/prof_c4.err"; exit 1; }
     find "$out/prof_c4" -name '*kernel_stats.csv' -exec cat {} \; ;;
   prof_c3)   # the checker launch alone (C4 shrunk to 1024 puzzles)

@@ -6,13 +6,16 @@ descriptions (rocprofv3 --list-avail) and checked against the kernel wall time:
   * SQ_CYCLES is summed over the shader engines (32 on MI355X: SQ_CYCLES / (wall x clock) = 32);
     an SE holds 8 CUs = 32 SIMDs, so SIMD quad-cycles = SQ_CYCLES / 4 x 32 and CU-cycles =
     SQ_CYCLES x 8;
-  * a wave64 VALU instruction occupies its SIMD's VALU issue for one quad-cycle
-    (SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU), and SQ_ACTIVE_INST_VALU2 counts the quad-cycles in
-    which a SIMD issued TWO VALU instructions.  So the quad-cycles with VALU issue are
+  * a wave64 VALU instruction issues over 2 cycles on a SIMD-32 (MI355X_MICROARCH.md:54), so the
+    issue peak is 2 per SIMD quad-cycle.  SQ_ACTIVE_INST_VALU2 counts the quad-cycles in which a
+    SIMD issued TWO VALU instructions, so the quad-cycles with any VALU issue are
     INSTS_VALU - VALU2, and
+      valu_per_quad    = SQ_INSTS_VALU / SIMD quad-cycles (the peak: 2.0)
       valu_busy_frac   = (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / SIMD quad-cycles
       valu_dual_frac   = SQ_ACTIVE_INST_VALU2 / SIMD quad-cycles
-      valu_per_quad    = SQ_INSTS_VALU / SIMD quad-cycles (2.0 would be dual issue every quad-cycle)
+    How much of the peak a kernel can use depends on its instruction mix: tools/issue_calib.hip
+    measures that (round 5: 2-operand VOP2 ops dual-issue in 78 % of quad-cycles, 3-source VOP3
+    and packed VOP3P ops in ~7 % and 0 %, so solve4's mix tops out near 1.05 per quad-cycle);
   * salu_per_cu_cycle = SQ_INSTS_SALU / CU-cycles; lds_busy_frac = SQ_LDS_IDX_ACTIVE / CU-cycles;
     lds_*_fifo_full_frac likewise; waves_per_simd = SQ_WAVE_CYCLES / SIMD quad-cycles;
   * clock_ghz = GRBM_GUI_ACTIVE / 8 / kernel wall (MI355X_MICROARCH.md "DVFS give-back").

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--sizes", default="1250000,10000000")
     ap.add_argument("--workload", default="solve17")
     ap.add_argument("--json", default="")
+    ap.add_argument("--order", default="lex", choices=["lex", "mrv_unique"])
     args = ap.parse_args()
     lib = L.load()
     fn = lib.sdk_debug_tl4
@@ -35,9 +36,16 @@ def main():
     with SudokuEngine(0) as eng:
         cus = eng.get_option(L.SDK_OPT_DEVICE_CUS)
         grid_max = cus * eng.get_option(L.SDK_OPT_WAVES_PER_CU2)
+        eng.set_option(L.SDK_OPT_DONATE, 0)          # one launch: the timeline of that launch
+        eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
         for n in [int(x) for x in args.sizes.split(",")]:
-            gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
-            p, s = gen(n, seed=11)
+            if args.workload == "hard":
+                p, s = synth.make_hard_sym(n, threads=16)
+            elif args.workload == "minimal":
+                p, s = synth.make_minimal_sym(n, threads=16)
+            else:
+                gen = synth.make_17clue if args.workload == "solve17" else synth.make_30clue
+                p, s = gen(n, seed=11)
             d_in, d_out, d_st = eng.alloc(n * 81), eng.alloc(n * 81), eng.alloc(n)
             d_in.upload(p)
             buf = (ctypes.c_ulonglong * (16384 * 4))()

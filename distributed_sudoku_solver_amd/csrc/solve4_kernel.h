@@ -553,10 +553,7 @@ struct Slot4 {
     uint32_t maxd;            // deepest DFS level reached (SDK_WORK_DEPTH)
     uint64_t nodes;
 };
-static __shared__ Slot4 s_slot4[4];
-#ifndef SDK_SOLVE4_STEAL
-#define SDK_SOLVE4_STEAL 1
-#endif
+static __shared__ Slot4 s_slot4[4];      // per-slot search state between steps: s_slot4[half * 2 + slot]
 
 __device__ __forceinline__ uint32_t cell_x4(uint32_t v) {
     return v == 0 ? kCands : 0u;
@@ -800,8 +797,6 @@ static __shared__ uint32_t s_dnepoch4;
 static __shared__ uint32_t s_dnfault4; // DnCtl.fault, read once at entry (registrations must not wait on it)
 static __shared__ uint32_t s_dngrid4;  // waves taking part (dn_grid4); the rest left at once
 static __shared__ uint32_t s_deq4;     // the wave's dequeue stage (next_board4)
-// per-slot search state between steps (Slot4, s_slot4[half * 2 + slot]); file scope so that a
-// slot whose queue ran dry can take boards from its half's other slot (next_board4)
 // the split phase's save area (split_save4), in LDS rather than kernel-argument SGPRs: it is read
 // only when a board is saved, and every SGPR live across the round loop is one the allocator may
 // spill into a VGPR lane (and then a round address to scratch)
@@ -1499,23 +1494,6 @@ __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, con
                 }
                 if (empty) base = (uint32_t)a.n;
                 if (w.hl == 0) atomicMax(&s_deq4, empty ? 2u : (drained ? 1u : 0u));
-                if (SDK_SOLVE4_STEAL && empty) {
-                    // the queue is dry: take the upper half of what the half's other slot still holds
-                    // after its current board (the rest of its last chunk; LDS only, no atomic).  A
-                    // wave ends when its slowest slot does, so at the end of a launch a slot that ran
-                    // dry while its sibling has boards queued behind the current one idles for them.
-                    // The other slot's state is in LDS (its steps are not running: they are HI ^ 1's),
-                    // and only this half touches its two slots.
-                    Slot4* o = s_slot4 + w.half * 2 + (HI ^ 1);
-                    const uint32_t ob = o->bidx, oe = o->bend;
-                    const uint32_t rest = (ob < (uint32_t)a.n && oe > ob + 1u) ? oe - ob - 1u : 0u;
-                    if (rest) {
-                        const uint32_t mid = oe - (rest + 1u) / 2u;
-                        if (w.hl == 0) o->bend = mid;
-                        base = mid;
-                        end = oe;
-                    }
-                }
             }
             b.bidx = min(base, (uint32_t)a.n);
             b.bend = min(base + (drained ? a.tail_chunk : a.chunk), end);

@@ -95,8 +95,25 @@ __global__ void dn_collect_kernel(const int8_t* status, uint64_t n, const uint32
                     const uint32_t depth = rs.save->hdr[e].y;
                     uint32_t items = 1;
                     for (uint32_t l = 0; l < depth; ++l) items += (uint32_t)__popc(rs.save->lv[e][l][0].y >> 23);
-                    if (atomicAdd(&rs.ctl->seed.res_boards, 1u) < kSeedBoards &&
-                        atomicAdd(&rs.ctl->seed.res_items, items) + items <= kSeedItems) {
+                    // reserve a board slot, then the items by compare-and-swap: a reservation is
+                    // committed only when it fits, and a board whose items do not fit gives its
+                    // slot back -- one deep stack does not use up the room of later small ones
+                    // (two unconditional adds consumed both on a failed reservation)
+                    bool fits = false;
+                    if (atomicAdd(&rs.ctl->seed.res_boards, 1u) < kSeedBoards) {
+                        uint32_t cur = __hip_atomic_load(&rs.ctl->seed.res_items, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                        while (cur + items <= kSeedItems) {
+                            const uint32_t prev = atomicCAS(&rs.ctl->seed.res_items, cur, cur + items);
+                            if (prev == cur) {
+                                fits = true;
+                                break;
+                            }
+                            cur = prev;
+                        }
+                    }
+                    if (!fits) atomicSub(&rs.ctl->seed.res_boards, 1u);
+                    if (fits) {
                         const uint32_t s = atomicAdd(rs.seeds, 1u);
                         rs.seeds[2 + 2 * s] = (uint32_t)i;
                         rs.seeds[3 + 2 * s] = e;
@@ -243,11 +260,25 @@ __global__ void dn_scatter_kernel(const uint32_t* list, const uint8_t* sub_out, 
 }
 }  // namespace sdk
 
+// Pinned host staging of the host-pointer calls (sdk_solve_batch_ex, sdk_expand_boards): the
+// caller's arrays are copied into it on the CPU and moved by true asynchronous DMA.  HIP's own path
+// for pageable memory took 12-25 ms per call now and then for a 1.3 MB transfer whose kernel ran
+// 0.2 ms (profiles/r05/slice_probe_timing_r05c.log: a node's search slices), all of it CPU time in
+// the calling thread.  Grown as needed up to kStageMax; larger calls keep the pageable path.
+struct HostBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+constexpr size_t kStageMax = size_t(256) << 20;
+constexpr size_t kStageInit = size_t(8) << 20;   // allocated with the context: pinning costs ~ms
+                                                 // (the first slice of a node paid 34 ms growing it)
+
 struct sdk_ctx {
     int device = 0;
     int cus = 256;
     hipStream_t stream = nullptr;
     std::mutex mu;
+    HostBuf stage;                 // pinned staging (see HostBuf)
     // options
     int order = SDK_ORDER_LEX;     // lex-first DFS: no uniqueness proof needed (faster than MRV_UNIQUE, r02)
     uint64_t budget = 0;
@@ -308,6 +339,23 @@ namespace {
 constexpr uint64_t kDnSplitDefault = 128;   // SDK_OPT_DONATE = 1: split budget (search nodes) of the plain phase
                                             // (256 to round 3; profiles/r03/sweep_split_r03.log)
 constexpr uint32_t kHeadRounds = 64;        // dequeue-head regions per clear (launch_solve_once)
+
+// a pinned staging area of at least `bytes` (nullptr: too large, use the pageable path)
+void* stage_host(HostBuf& b, size_t bytes) {
+    if (bytes > kStageMax) return nullptr;
+    if (b.bytes >= bytes) return b.p;
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    // doubling growth: a node's slices grow their batches a little at a time
+    const size_t want = std::min(kStageMax, std::max(bytes, std::max(b.bytes * 2, kStageInit)));
+    if (hipHostMalloc(&b.p, want, hipHostMallocDefault) != hipSuccess) {
+        b.p = nullptr;
+        return nullptr;
+    }
+    b.bytes = want;
+    return b.p;
+}
 
 int ensure(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes) return SDK_OK;
@@ -900,13 +948,26 @@ int expand_boards(sdk_ctx* c, const uint8_t* h_in, const uint16_t* h_masks, uint
     if (n > kFrontierCap) return fail(SDK_EINVAL, "at most %llu seed boards", (unsigned long long)kFrontierCap);
     int rc;
     if ((rc = ensure(c->fr_a, frontier_capacity(n, target) * 81)) || (rc = ensure(c->fr_mask, n * 2))) return rc;
-    HIPCALL(hipMemcpyAsync(c->fr_a.p, h_in, n * 81, hipMemcpyHostToDevice, c->stream));
-    if (h_masks) HIPCALL(hipMemcpyAsync(c->fr_mask.p, h_masks, n * 2, hipMemcpyHostToDevice, c->stream));
+    // through the pinned staging area (see HostBuf); run_frontier_levels synchronizes before returning
+    char* st = static_cast<char*>(stage_host(c->stage, n * 83));
+    if (st) {
+        std::memcpy(st, h_in, n * 81);
+        if (h_masks) std::memcpy(st + n * 81, h_masks, n * 2);
+    }
+    HIPCALL(hipMemcpyAsync(c->fr_a.p, st ? st : (const char*)h_in, n * 81, hipMemcpyHostToDevice, c->stream));
+    if (h_masks)
+        HIPCALL(hipMemcpyAsync(c->fr_mask.p, st ? st + n * 81 : (const char*)h_masks, n * 2, hipMemcpyHostToDevice,
+                               c->stream));
     if ((rc = run_frontier_levels(c, n, h_masks != nullptr, SDK_FRONTIER_FIRST, target, true))) return rc;
     if (c->fr_size > cap)
         return fail(SDK_EINVAL, "frontier of %llu boards exceeds cap %llu (pass cap >= 9 * max(n, target))",
                     (unsigned long long)c->fr_size, (unsigned long long)cap);
-    if (c->fr_size) HIPCALL(hipMemcpyAsync(h_out, c->fr_a.p, c->fr_size * 81, hipMemcpyDeviceToHost, c->stream));
+    if (c->fr_size) {
+        char* so = static_cast<char*>(stage_host(c->stage, c->fr_size * 81));
+        HIPCALL(hipMemcpyAsync(so ? so : (char*)h_out, c->fr_a.p, c->fr_size * 81, hipMemcpyDeviceToHost, c->stream));
+        HIPCALL(hipStreamSynchronize(c->stream));
+        if (so) std::memcpy(h_out, so, c->fr_size * 81);
+    }
     HIPCALL(hipStreamSynchronize(c->stream));
     *out_n = c->fr_size;
     return SDK_OK;
@@ -1029,6 +1090,7 @@ int sdk_create(int device, sdk_ctx** out) {
         delete c;
         return fail(SDK_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
+    (void)stage_host(c->stage, kStageInit);   // best effort: a failure leaves the pageable path
     *out = c;
     return SDK_OK;
 }
@@ -1044,6 +1106,7 @@ int sdk_destroy(sdk_ctx* c) {
                       &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status,
                       &c->fr_mask, &c->tsum, &c->fr_ctl})
         if (b->p) (void)hipFree(b->p);
+    if (c->stage.p) (void)hipHostFree(c->stage.p);
     for (auto& pr : c->events) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -1415,17 +1478,33 @@ int sdk_solve_batch_ex(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell
     if ((rc = ensure(c->in, n * 81)) || (rc = ensure(c->out, n * 81)) || (rc = ensure(c->status, n))) return rc;
     if (first_cell_mask && (rc = ensure(c->mask, n * 2))) return rc;
     if (work && (rc = ensure(c->work, n * 8))) return rc;
-    HIPCALL(hipMemcpyAsync(c->in.p, in, n * 81, hipMemcpyHostToDevice, c->stream));
-    if (first_cell_mask) HIPCALL(hipMemcpyAsync(c->mask.p, first_cell_mask, n * 2, hipMemcpyHostToDevice, c->stream));
+    // staging layout: work (n x 8), masks (n x 2), in / out boards (n x 81), status (n)
+    char* st = static_cast<char*>(stage_host(c->stage, n * (8 + 2 + 81 + 1)));
+    uint64_t* s_work = reinterpret_cast<uint64_t*>(st);
+    uint16_t* s_mask = st ? reinterpret_cast<uint16_t*>(st + n * 8) : nullptr;
+    uint8_t* s_io = st ? reinterpret_cast<uint8_t*>(st + n * 10) : nullptr;
+    int8_t* s_st = st ? reinterpret_cast<int8_t*>(st + n * 91) : nullptr;
+    if (st) {
+        std::memcpy(s_io, in, n * 81);
+        if (first_cell_mask) std::memcpy(s_mask, first_cell_mask, n * 2);
+    }
+    HIPCALL(hipMemcpyAsync(c->in.p, st ? s_io : in, n * 81, hipMemcpyHostToDevice, c->stream));
+    if (first_cell_mask)
+        HIPCALL(hipMemcpyAsync(c->mask.p, st ? s_mask : first_cell_mask, n * 2, hipMemcpyHostToDevice, c->stream));
     rc = launch_solve(c, static_cast<uint8_t*>(c->in.p), first_cell_mask ? static_cast<uint16_t*>(c->mask.p) : nullptr,
                       static_cast<uint8_t*>(c->out.p), static_cast<int8_t*>(c->status.p),
                       work ? static_cast<uint64_t*>(c->work.p) : nullptr, n, 0, 0, nullptr, nullptr, 0, 1, -1,
                       node_budget == SDK_BUDGET_CONTEXT ? -1 : (int64_t)node_budget, donate);
     if (rc) return rc;
-    HIPCALL(hipMemcpyAsync(out, c->out.p, n * 81, hipMemcpyDeviceToHost, c->stream));
-    HIPCALL(hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
-    if (work) HIPCALL(hipMemcpyAsync(work, c->work.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipMemcpyAsync(st ? s_io : out, c->out.p, n * 81, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipMemcpyAsync(st ? s_st : status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+    if (work) HIPCALL(hipMemcpyAsync(st ? s_work : work, c->work.p, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCALL(hipStreamSynchronize(c->stream));
+    if (st) {
+        std::memcpy(out, s_io, n * 81);
+        std::memcpy(status, s_st, n);
+        if (work) std::memcpy(work, s_work, n * 8);
+    }
     return dn_check_error(c);
 }
 

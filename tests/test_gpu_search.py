@@ -163,13 +163,11 @@ def test_node_slices_are_bounded(engine):
             # per node of a launch's critical path stays within LAUNCH_SHARE of the target
             assert s.budget == 1 or s.budget * s.t_node <= LAUNCH_SHARE * SLICE_TARGET_S * 1.001, (s.budget, s.t_node)
         assert not s.done
-        # measured: the slices themselves.  A box-wide stall (every part of one slice -- launch,
-        # expansion and the host's own numpy work -- slowed about 20x at once, ~1 slice in 75 in
-        # profiles/r04/slice_probe_node.log) is not the search's budget, so the bound is asserted
-        # on the median and the 90th percentile
-        srt = sorted(times)
-        assert srt[len(srt) // 2] <= SLICE_TARGET_S and srt[int(0.9 * len(srt))] <= 1.5 * SLICE_TARGET_S, \
-            (["%.2f" % (1e3 * t) for t in times], s.budget, s.width)
+        # measured: the slices themselves, every one.  The slow slices of round 4 (12-27 ms, kernel
+        # 0.2-2 ms) were HIP's pageable-memory path in the calling thread; the host-pointer calls
+        # now stage through pinned memory (sudoku_hip.hip, HostBuf) and the worst of 199 slices
+        # after the first was 5.6 ms (profiles/r05/slice_probe_timing_r05d.log)
+        assert max(times) <= 1.5 * SLICE_TARGET_S, (["%.2f" % (1e3 * t) for t in times], s.budget, s.width)
         assert s.budget > 1                            # the bound leaves room to search
     finally:
         fork.close()

@@ -50,6 +50,10 @@ SDK_OPT_DN_FAULT = 21
 SDK_OPT_DONATE_HELPERS = 22
 SDK_OPT_DONATE_RESUME = 23
 SDK_OPT_RESUMED = 24
+SDK_OPT_PROP32 = 25
+SDK_OPT_PROP32_LC = 26
+SDK_OPT_PROP32_MIN = 27
+SDK_OPT_PROP32_UNDECIDED = 28
 SDK_DONATE_CONTEXT = -1    # sdk_solve_batch_ex: use the context's SDK_OPT_DONATE
 SDK_CHECK_REG1 = 0
 SDK_CHECK_REG2 = 1

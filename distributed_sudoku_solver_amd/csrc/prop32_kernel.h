@@ -1,0 +1,550 @@
+// prop32_kernel.h -- root propagation of 32 boards per half-wave, bit-sliced: the QUAD solver's
+// first pass over a batch ("prop32").
+//
+// What it decides.  The reference solves every board by depth-first search (DHT_Node.py:512-535,
+// `solve_sudoku`); a board whose constraint propagation alone -- naked and hidden singles, pointing
+// and claiming (locked candidates) -- fills every cell has exactly one completion, so every
+// search order returns it: status 1 and that grid.  One that propagation refutes has none: status 0
+// and the input grid back (DHT_Node.py:535).  Everything else -- a board propagation leaves open,
+// a board with a duplicated or out-of-domain given (whose units are not "exact", see solve4_kernel.h
+// unit4x), a board still changing after max_steps -- is left undecided (kStUndecided): it goes to
+// the fallback list with its input, solve4_kernel searches it from scratch, and its answer is
+// scattered back (sudoku_hip.hip, launch_solve).  On the 17-clue workload of the headline metric
+// every board is decided here (tools/lockstep_model.py: all of 2,048 solved by propagation).
+//
+// Layout.  Bit b of a 32-bit word is board b of the half's group of 32 (board base + 32 * half + b).
+// Lane hl < 27 of a half owns cells hl, hl + 27, hl + 54 -- as in solve4 -- with nine candidate
+// words per cell (c[k][d], bit b set: digit d + 1 is still possible in that cell of board b) and
+// unit hl (rows 0-8, columns 9-17, boxes 18-26).  A cell is closed when exactly one candidate is
+// left (its single word s[k]); no separate closed state.  Lanes 27..31 run the same code on spare
+// slots (their results are masked out).
+//
+// One step for all 32 boards of a half:
+//   singles:  s = exactly-one over the nine words, empty = no candidate, and the cell records
+//             (9 candidate words + s) written to LDS;
+//   unit:     the lane's unit over its nine cell records -- T (digits of its closed cells),
+//             once (digits in exactly one cell), missing digits (contradiction) -- written as
+//             (T_d, once_d) pairs;
+//   cells:    each cell loses the T of its three units unless closed, takes a hidden single
+//             (a remaining candidate in some unit's once), and "changed" is accumulated.
+// Every lc_every-th step (and whenever every live board is at a fixpoint) the unit/cell phases
+// are replaced by one locked-candidates pass over the 54 box-line triads:
+//   presence P(triad) = OR of its three cells' words (closed cells included, so the pass is sound at
+//   any state); claim(L,B) = P(L,B) & ~P(L,B1) & ~P(L,B2); point(L,B) = P(L,B) & ~P(L1,B) & ~P(L2,B);
+//   a triad's open cells lose claim(L1,B) | claim(L2,B) | point(L,B1) | point(L,B2).
+// A board whose last singles step changed nothing and whose locked-candidates pass removes nothing
+// is stuck: undecided.
+//
+// The two halves run their groups in lock step (one instruction stream, no divergence): a wave
+// takes 64 boards per dequeue and steps until no board of either half is live.
+//
+// The exact-unit argument of solve4_kernel.h unit4x carries over: with no duplicated and no
+// out-of-domain given, a digit taken twice in a unit leaves another digit of the unit without a
+// cell, so the missing-digit test refutes every such state -- a board is declared solved only when
+// every cell is closed and no unit misses a digit (then each unit holds each digit once).
+#pragma once
+#include "solve_kernel.h"
+
+namespace sdk {
+
+// status of a board the propagation pass left to the search (never returned to callers)
+constexpr int kStUndecided = -4;
+
+constexpr uint32_t kP32Rec = 40;         // bytes per cell record: 9 candidate words, the single word
+constexpr uint32_t kP32URec = 72;        // bytes per unit record: (T_d, once_d), d = 0..8
+constexpr uint32_t kP32TRec = 40;        // bytes per triad record: 9 words + pad
+constexpr uint32_t kP32ColTri = 1280;    // the column triads' records (32 row-triad slots before)
+constexpr uint32_t kP32Region = 3456;    // bytes per half: 86 cell records (81 + the spare lanes')
+constexpr uint32_t kP32Stage = 2592;     // bytes per half of the group's boards (32 x 81)
+constexpr uint32_t kP32Heads = 8;        // dequeue counters, one per XCD segment of the groups
+constexpr uint32_t kP32HeadStride = 32;  // words between counters (own cache lines)
+
+struct Prop32Args {
+    const uint8_t* in;       // boards [n][81]; 16-byte aligned
+    uint8_t* out;            // [n][81]; 16-byte aligned
+    int8_t* status;          // [n]: 1 solved, 0 no completion, kStUndecided
+    uint64_t n;
+    uint32_t* heads;         // kP32Heads counters kP32HeadStride words apart (zeroed)
+    uint32_t* list;          // [0] undecided boards, then their indices (list[0] zeroed)
+    uint8_t* list_in;        // the undecided boards' inputs, dense, in list order
+    uint32_t lc_every;       // a locked-candidates pass every lc_every-th step
+    uint32_t max_steps;      // boards still live after this many steps are undecided
+};
+
+// OR / AND over the 32 lanes of each half, result in every lane of the half: rotations inside
+// each row of 16 (DPP), then lane ^ 16 (ds_swizzle, bit-mask mode: and 0x1F, xor 0x10).  Every
+// lane of the wave must be active.
+__device__ __forceinline__ uint32_t p32_half_or(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xF, 0xF, false);   // row_ror:1
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xF, 0xF, false);   // row_ror:2
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, false);   // row_ror:4
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);   // row_ror:8
+    x |= (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);
+    return x;
+}
+__device__ __forceinline__ uint32_t p32_half_and(uint32_t x) { return ~p32_half_or(~x); }
+
+// LDS access through address-space-3 pointers (ds_* instructions); loads are volatile so the
+// compiler keeps them single ds_read_b64 (a ds_read2_b64 pair costs 8 LDS-array cycles against
+// 2 x 2, MI355X_MICROARCH.md LDS table)
+typedef __attribute__((address_space(3))) uint8_t p32_lds_t;
+typedef unsigned int p32_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint2 p32_ld(p32_lds_t* base, uint32_t off) {
+    const uint64_t v = *(const volatile __attribute__((address_space(3))) uint64_t*)(base + off);
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+__device__ __forceinline__ void p32_st(p32_lds_t* base, uint32_t off, uint32_t x, uint32_t y) {
+    *(__attribute__((address_space(3))) uint64_t*)(base + off) = (uint64_t)x | ((uint64_t)y << 32);
+}
+
+// a copy of v the compiler cannot see through: per-lane addresses derived from it are computed
+// where they are used instead of being hoisted out of the step loop (where they would hold ~20
+// VGPRs for the whole kernel)
+__device__ __forceinline__ uint32_t p32_opq(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+struct P32Lane {
+    uint32_t half, hl;
+    bool act;
+    p32_lds_t* reg;        // the half's LDS region
+};
+
+struct P32Cells {
+    uint32_t c[3][9];
+    uint32_t s[3];
+};
+
+// singles: s = exactly one candidate, empty = none; the cell records of the real lanes (cell j at
+// 40j: cells hl + 27k at 40 hl + 1080k)
+__device__ __forceinline__ void p32_singles(const P32Lane& w, P32Cells& x, uint32_t& empty, uint32_t& alls) {
+    empty = 0u;
+    alls = ~0u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        uint32_t a1 = x.c[k][0], a2 = 0u;
+#pragma unroll
+        for (int d = 1; d < 9; ++d) {
+            a2 |= a1 & x.c[k][d];
+            a1 |= x.c[k][d];
+        }
+        x.s[k] = a1 & ~a2;
+        empty |= ~a1;
+        alls &= x.s[k];
+    }
+    if (!w.act) return;   // spare lanes store nothing: their reads below return whatever is there
+    const uint32_t rec = kP32Rec * p32_opq(w.hl);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t o = rec + 1080u * k;
+        p32_st(w.reg, o, x.c[k][0], x.c[k][1]);
+        p32_st(w.reg, o + 8, x.c[k][2], x.c[k][3]);
+        p32_st(w.reg, o + 16, x.c[k][4], x.c[k][5]);
+        p32_st(w.reg, o + 24, x.c[k][6], x.c[k][7]);
+        p32_st(w.reg, o + 32, x.c[k][8], x.s[k]);
+    }
+}
+
+// the unit summary of the lane's unit (rows 0-8, columns 9-17, boxes 18-26); FIRST (a group's
+// first step: closed cells are the givens) also reports digits given twice (dup: not exact)
+template <bool FIRST>
+__device__ __forceinline__ void p32_unit(const P32Lane& w, uint32_t& miss, uint32_t& dup) {
+    const uint32_t j = p32_opq(w.hl);
+    // cell q of the unit at u0 + (q % 3) ua + (q / 3) ub
+    uint32_t u0, ua, ub;
+    if (j < 9) {                           // row j: cells 9j + q
+        u0 = kP32Rec * 9 * j; ua = kP32Rec; ub = 3 * kP32Rec;
+    } else if (j < 18) {                   // column j - 9: cells 9q + (j - 9)
+        u0 = kP32Rec * (j - 9); ua = 9 * kP32Rec; ub = 27 * kP32Rec;
+    } else if (j < 27) {                   // box b: rows 3 (b / 3) + q / 3, columns 3 (b % 3) + q % 3
+        const uint32_t b = j - 18;
+        u0 = kP32Rec * (27 * (b / 3) + 3 * (b % 3)); ua = kP32Rec; ub = 9 * kP32Rec;
+    } else {                               // spare lane: one unwritten record, nine times
+        u0 = kP32Rec * (54 + j); ua = 0; ub = 0;
+    }
+    uint32_t ones[9], twos[9], T[9];
+    dup = 0u;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+        const uint32_t o = u0 + (uint32_t)(q % 3) * ua + (uint32_t)(q / 3) * ub;
+        const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
+                    r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
+        const uint32_t a[9] = {r0.x, r0.y, r1.x, r1.y, r2.x, r2.y, r3.x, r3.y, r4.x};
+        const uint32_t s = r4.y;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            if (q == 0) {
+                ones[d] = a[d];
+                twos[d] = 0u;
+                T[d] = a[d] & s;
+            } else {
+                if (FIRST) dup |= T[d] & a[d] & s;
+                twos[d] |= ones[d] & a[d];
+                ones[d] |= a[d];
+                T[d] |= a[d] & s;
+            }
+        }
+        // one cell's reads at a time: the accumulators pass through here, so the next cell's loads
+        // cannot be hoisted above this cell's arithmetic (left alone the scheduler issues all 45
+        // loads first and spills)
+        asm volatile("" : "+v"(ones[0]), "+v"(ones[1]), "+v"(ones[2]), "+v"(ones[3]), "+v"(ones[4]), "+v"(ones[5]),
+                     "+v"(ones[6]), "+v"(ones[7]), "+v"(ones[8]), "+v"(twos[0]), "+v"(twos[1]), "+v"(twos[2]),
+                     "+v"(twos[3]), "+v"(twos[4]), "+v"(twos[5]), "+v"(twos[6]), "+v"(twos[7]), "+v"(twos[8]),
+                     "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]), "+v"(T[6]),
+                     "+v"(T[7]), "+v"(T[8])::"memory");
+    }
+    miss = 0u;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) miss |= ~ones[d];
+    __builtin_amdgcn_wave_barrier();   // every lane's reads before the records are overwritten
+    const uint32_t urec = kP32URec * j;   // spare lanes: unit slots 27..31
+#pragma unroll
+    for (int d = 0; d < 9; ++d) p32_st(w.reg, urec + 8 * d, T[d], ones[d] & ~twos[d]);
+}
+
+// the cell update of one step; returns the change bits of the lane's three cells
+__device__ __forceinline__ uint32_t p32_cells(const P32Lane& w, P32Cells& x) {
+    const uint32_t j = p32_opq(w.hl);
+    const uint32_t r0 = j / 9, col = j - 9 * r0;      // cells j + 27k: row r0 + 3k, column col
+    const uint32_t colrec = kP32URec * (9 + col), rowrec = kP32URec * r0, boxrec = kP32URec * (18 + col / 3);
+    uint32_t cT[9], cH[9];
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+        const uint2 v = p32_ld(w.reg, colrec + 8 * d);
+        cT[d] = v.x;
+        cH[d] = v.y;
+    }
+    uint32_t chg = 0u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        uint32_t H[9], anyh = 0u;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            const uint2 r = p32_ld(w.reg, rowrec + 216u * k + 8 * d);   // row r0 + 3k
+            const uint2 b = p32_ld(w.reg, boxrec + 216u * k + 8 * d);   // box 3k + col / 3
+            const uint32_t U = cT[d] | r.x | b.x;
+            H[d] = cH[d] | r.y | b.y;
+            const uint32_t v1 = x.c[k][d] & (~U | x.s[k]);   // a closed cell keeps its digit
+            chg |= x.c[k][d] & ~v1;
+            anyh |= v1 & H[d];
+            x.c[k][d] = v1;
+        }
+        // a hidden single: v2 = h | (v1 & ~anyh) = v1 & (H | ~anyh)
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            const uint32_t v2 = x.c[k][d] & (H[d] | ~anyh);
+            chg |= x.c[k][d] & ~v2;
+            x.c[k][d] = v2;
+        }
+    }
+    return chg;
+}
+
+// the eliminations into the lane's triad (line tl, box index tb along the line) of one kind
+// (base: the row or column triads' records): lines L1, L2 of the band / stack, boxes B1, B2
+__device__ __forceinline__ void p32_elim(const P32Lane& w, uint32_t tl, uint32_t tb, uint32_t base,
+                                         uint32_t (&e)[9]) {
+    const uint32_t L0 = tl - tl % 3;
+    const uint32_t L1 = L0 + (tl - L0 + 1) % 3, L2 = L0 + (tl - L0 + 2) % 3;
+    const uint32_t B1 = (tb + 1) % 3, B2 = (tb + 2) % 3;
+    const uint32_t oL1B = base + kP32TRec * (3 * L1 + tb), oL1B1 = base + kP32TRec * (3 * L1 + B1),
+                   oL1B2 = base + kP32TRec * (3 * L1 + B2), oL2B = base + kP32TRec * (3 * L2 + tb),
+                   oL2B1 = base + kP32TRec * (3 * L2 + B1), oL2B2 = base + kP32TRec * (3 * L2 + B2),
+                   oLB1 = base + kP32TRec * (3 * tl + B1), oLB2 = base + kP32TRec * (3 * tl + B2);
+#pragma unroll
+    for (int h = 0; h < 5; ++h) {
+        const uint2 l1b = p32_ld(w.reg, oL1B + 8 * h), l1b1 = p32_ld(w.reg, oL1B1 + 8 * h),
+                    l1b2 = p32_ld(w.reg, oL1B2 + 8 * h), l2b = p32_ld(w.reg, oL2B + 8 * h),
+                    l2b1 = p32_ld(w.reg, oL2B1 + 8 * h), l2b2 = p32_ld(w.reg, oL2B2 + 8 * h),
+                    lb1 = p32_ld(w.reg, oLB1 + 8 * h), lb2 = p32_ld(w.reg, oLB2 + 8 * h);
+        e[2 * h] = (l1b.x & ~(l1b1.x | l1b2.x)) | (l2b.x & ~(l2b1.x | l2b2.x)) |
+                   (lb1.x & ~(l1b1.x | l2b1.x)) | (lb2.x & ~(l1b2.x | l2b2.x));
+        if (h < 4)
+            e[2 * h + 1] = (l1b.y & ~(l1b1.y | l1b2.y)) | (l2b.y & ~(l2b1.y | l2b2.y)) |
+                           (lb1.y & ~(l1b1.y | l2b1.y)) | (lb2.y & ~(l1b2.y | l2b2.y));
+    }
+}
+
+// one locked-candidates pass (the cell records of this step are in LDS); returns the change bits.
+// Lane j < 27 owns row triad j (row j / 3, box column j % 3) and column triad j (column j / 3,
+// box row j % 3); spare lanes read triad 26's cells and write their own slots 27..31.
+__device__ __forceinline__ uint32_t p32_locked(const P32Lane& w, P32Cells& x) {
+    const uint32_t j = p32_opq(w.hl), jt = min(j, 26u);
+    const uint32_t tl = jt / 3, tb = jt - 3 * tl;
+    const uint32_t rtri = kP32Rec * (9 * tl + 3 * tb), ctri = kP32Rec * (27 * tb + tl);
+    const uint32_t rtrec = kP32TRec * j, ctrec = kP32ColTri + kP32TRec * j;
+    // presence of the lane's row triad and column triad
+    uint32_t pr[9], pc[9];
+#pragma unroll
+    for (int h = 0; h < 5; ++h) {
+        const uint2 a0 = p32_ld(w.reg, rtri + 8 * h), a1 = p32_ld(w.reg, rtri + 40 + 8 * h),
+                    a2 = p32_ld(w.reg, rtri + 80 + 8 * h);
+        const uint2 b0 = p32_ld(w.reg, ctri + 8 * h), b1 = p32_ld(w.reg, ctri + 360 + 8 * h),
+                    b2 = p32_ld(w.reg, ctri + 720 + 8 * h);
+        pr[2 * h] = a0.x | a1.x | a2.x;
+        pc[2 * h] = b0.x | b1.x | b2.x;
+        if (h < 4) {
+            pr[2 * h + 1] = a0.y | a1.y | a2.y;
+            pc[2 * h + 1] = b0.y | b1.y | b2.y;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < 5; ++h) {
+        p32_st(w.reg, rtrec + 8 * h, pr[2 * h], h < 4 ? pr[2 * h + 1] : 0u);
+        p32_st(w.reg, ctrec + 8 * h, pc[2 * h], h < 4 ? pc[2 * h + 1] : 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t er[9], ec[9];
+    p32_elim(w, tl, tb, 0u, er);
+    p32_elim(w, tl, tb, kP32ColTri, ec);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < 5; ++h) {
+        p32_st(w.reg, rtrec + 8 * h, er[2 * h], h < 4 ? er[2 * h + 1] : 0u);
+        p32_st(w.reg, ctrec + 8 * h, ec[2 * h], h < 4 ? ec[2 * h + 1] : 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // apply to the lane's open cells: cell j + 27k lies in row triad 3 (r0 + 3k) + col / 3 and
+    // column triad 3 col + k
+    const uint32_t r0 = j / 9, col = j - 9 * r0;
+    const uint32_t at_r = kP32TRec * (3 * r0 + col / 3), at_c = kP32ColTri + kP32TRec * (3 * col);
+    uint32_t chg = 0u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+        for (int h = 0; h < 5; ++h) {
+            const uint2 r = p32_ld(w.reg, at_r + 360u * k + 8 * h);
+            const uint2 c = p32_ld(w.reg, at_c + 40u * k + 8 * h);
+            {
+                const uint32_t rm = (r.x | c.x) & x.c[k][2 * h] & ~x.s[k];
+                chg |= rm;
+                x.c[k][2 * h] ^= rm;
+            }
+            if (h < 4) {
+                const uint32_t rm = (r.y | c.y) & x.c[k][2 * h + 1] & ~x.s[k];
+                chg |= rm;
+                x.c[k][2 * h + 1] ^= rm;
+            }
+        }
+    }
+    return chg;
+}
+
+// the 64-bit board mask of a half-reduced word (lane 0: boards 0..31, lane 32: boards 32..63)
+__device__ __forceinline__ uint64_t p32_mask64(uint32_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// the next group of 64 boards: the home segment's counter (blockIdx % kP32Heads, one XCD), then
+// the others in turn.  Returns the group index or ~0u.
+__device__ __forceinline__ uint32_t p32_dequeue(const Prop32Args& a, uint32_t groups, uint32_t& seg) {
+    const uint32_t per = (groups + kP32Heads - 1) / kP32Heads;
+    for (uint32_t t = 0; t < kP32Heads; ++t) {
+        const uint32_t sg = (seg + t) % kP32Heads;
+        const uint32_t lo = sg * per, hi = min(lo + per, groups);
+        if (lo >= hi) continue;
+        uint32_t g = 0;
+        if (threadIdx.x == 0) {
+            // a drained segment: one plain read instead of an atomic that only counts further
+            g = __hip_atomic_load(a.heads + sg * kP32HeadStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lo + g < hi) g = atomicAdd(a.heads + sg * kP32HeadStride, 1u);
+        }
+        g = lo + (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+        if (g < hi) {
+            seg = sg;
+            return g;
+        }
+    }
+    return ~0u;
+}
+
+#ifdef SDK_DEFINE_PROP32_KERNEL
+#ifndef SDK_PROP32_WAVES_PER_EU
+#define SDK_PROP32_WAVES_PER_EU 5
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_WAVES_PER_EU))) void prop32_kernel(
+    Prop32Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[2 * kP32Region];
+    p32_lds_t* const lds = (p32_lds_t*)s_lds;
+    P32Lane w;
+    w.half = threadIdx.x >> 5;
+    w.hl = threadIdx.x & 31;
+    w.act = w.hl < 27;
+    w.reg = lds + w.half * kP32Region;
+    const uint32_t groups = (uint32_t)((a.n + 63) / 64);
+    uint32_t seg = blockIdx.x % kP32Heads;
+    for (;;) {
+        const uint32_t g = p32_dequeue(a, groups, seg);
+        if (g == ~0u) break;
+        const uint64_t base = (uint64_t)g * 64;
+        const uint32_t nb = (uint32_t)min<uint64_t>(64, a.n - base);
+        // the group's boards into the staging (row-major, 81 bytes each; half h: boards 32h..)
+        const uint8_t* src = a.in + base * 81;
+        if (nb == 64) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const uint32_t q = threadIdx.x + 64u * i;
+                if (q < 324u) {
+                    const p32_u4 v = reinterpret_cast<const p32_u4*>(src)[q];
+                    const uint32_t o = 16u * q, h = o >= kP32Stage ? 1u : 0u;
+                    *(__attribute__((address_space(3))) p32_u4*)(lds + h * kP32Region + o - h * kP32Stage) = v;
+                }
+            }
+        } else {
+            for (uint32_t o = threadIdx.x; o < nb * 81u; o += 64u) {
+                const uint32_t h = o >= kP32Stage ? 1u : 0u;
+                lds[h * kP32Region + o - h * kP32Stage] = src[o];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // bit-sliced candidate words: digit v -> one word, 0 -> all nine, > 9 -> inert (undecided)
+        P32Cells x;
+        uint32_t inert = 0u;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int d = 0; d < 9; ++d) x.c[k][d] = 0u;
+#pragma unroll 2
+        for (uint32_t b = 0; b < 32; ++b) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t v = w.reg[b * 81u + w.hl + 27u * k];
+                const uint32_t m = v == 0u ? 0x1FFu : (v <= 9u ? 1u << (v - 1u) : 0u);
+                inert |= (v > 9u ? 1u : 0u) << b;
+#pragma unroll
+                for (int d = 0; d < 9; ++d) x.c[k][d] |= ((m >> d) & 1u) << b;
+            }
+        }
+        // per-group bookkeeping as 64-bit board masks in scalar registers (bit 32h + b: board b of
+        // half h)
+        const uint64_t valid = nb >= 64u ? ~0ull : ((1ull << nb) - 1ull);
+        uint64_t undec = p32_mask64(p32_half_or(w.act ? inert : 0u)) & valid;
+        uint64_t live = valid & ~undec, solved = 0ull, contra = 0ull, fixw = 0ull;
+        bool lc = false;
+        for (uint32_t it = 0;;) {
+            uint32_t empty, alls;
+            p32_singles(w, x, empty, alls);
+            __builtin_amdgcn_wave_barrier();
+            if (lc) {
+                const uint32_t lc_own = p32_locked(w, x);
+                const uint64_t lchg = p32_mask64(p32_half_or(w.act ? lc_own : 0u));
+                const uint64_t stuck = fixw & ~lchg & live;
+                undec |= stuck;
+                live &= ~stuck;
+                fixw = 0ull;
+                lc = false;
+                if (live == 0ull) break;
+                __builtin_amdgcn_wave_barrier();
+                continue;
+            }
+            uint32_t miss, dup;
+            if (it == 0)
+                p32_unit<true>(w, miss, dup);
+            else
+                p32_unit<false>(w, miss, dup);
+            const uint64_t badw = p32_mask64(p32_half_or(w.act ? (miss | empty) : 0u));
+            const uint64_t allw = p32_mask64(p32_half_and(w.act ? alls : ~0u));
+            if (it == 0) {
+                const uint64_t dupw = p32_mask64(p32_half_or(w.act ? dup : 0u)) & live;
+                undec |= dupw;
+                live &= ~dupw;
+            }
+            const uint64_t sv = allw & ~badw & live, ct = badw & live;
+            solved |= sv;
+            contra |= ct;
+            live &= ~(sv | ct);
+            if (live == 0ull) break;
+            if (++it >= a.max_steps) {
+                undec |= live;
+                break;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t chg_own = p32_cells(w, x);
+            const uint64_t chgw = p32_mask64(p32_half_or(w.act ? chg_own : 0u));
+            fixw = live & ~chgw;
+            // the next step is a locked-candidates pass every lc_every-th step, and whenever every
+            // live board is at a singles fixpoint
+            lc = (it % a.lc_every) == 0u || fixw == live;
+            __builtin_amdgcn_wave_barrier();
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the answers, in the staging: solved boards' digits (binary planes of the one-hot words),
+        // boards without a completion their input (DHT_Node.py:535); then out, for the whole group
+        if (solved) {
+            uint32_t p0[3], p1[3], p2[3], p3[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                p0[k] = x.c[k][0] | x.c[k][2] | x.c[k][4] | x.c[k][6] | x.c[k][8];
+                p1[k] = x.c[k][1] | x.c[k][2] | x.c[k][5] | x.c[k][6];
+                p2[k] = x.c[k][3] | x.c[k][4] | x.c[k][5] | x.c[k][6];
+                p3[k] = x.c[k][7] | x.c[k][8];
+            }
+            if (w.act) {
+#pragma unroll 2
+                for (uint32_t b = 0; b < 32; ++b) {
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const uint32_t v = ((p0[k] >> b) & 1u) | (((p1[k] >> b) & 1u) << 1) |
+                                           (((p2[k] >> b) & 1u) << 2) | (((p3[k] >> b) & 1u) << 3);
+                        w.reg[b * 81u + w.hl + 27u * k] = (uint8_t)v;
+                    }
+                }
+            }
+        }
+        for (uint64_t m = contra; m; m &= m - 1ull) {     // rare: the 81 bytes by 64 lanes
+            const uint32_t p = (uint32_t)__builtin_ctzll(m);
+            const uint8_t* s = a.in + (base + p) * 81;
+            p32_lds_t* d = lds + (p >> 5) * kP32Region + (p & 31u) * 81u;
+            d[threadIdx.x] = s[threadIdx.x];
+            if (threadIdx.x < 17u) d[64 + threadIdx.x] = s[64 + threadIdx.x];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (solved | contra) {
+            // undecided boards' rows get what the staging holds; the search's answers replace them
+            uint8_t* dst = a.out + base * 81;
+            if (nb == 64) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const uint32_t q = threadIdx.x + 64u * i;
+                    if (q < 324u) {
+                        const uint32_t o = 16u * q, h = o >= kP32Stage ? 1u : 0u;
+                        reinterpret_cast<p32_u4*>(dst)[q] =
+                            *(const __attribute__((address_space(3))) p32_u4*)(lds + h * kP32Region + o - h * kP32Stage);
+                    }
+                }
+            } else {
+                for (uint32_t o = threadIdx.x; o < nb * 81u; o += 64u) {
+                    const uint32_t h = o >= kP32Stage ? 1u : 0u;
+                    dst[o] = lds[h * kP32Region + o - h * kP32Stage];
+                }
+            }
+        }
+        // statuses; the undecided boards are listed with their inputs for the search
+        const uint32_t me = threadIdx.x;                  // board me of the group (32 half + hl)
+        if ((valid >> me) & 1ull)
+            a.status[base + me] = (int8_t)(((solved >> me) & 1ull) ? 1 : (((contra >> me) & 1ull) ? 0 : kStUndecided));
+        if (undec) {
+            uint32_t k0 = 0;
+            if (threadIdx.x == 0) k0 = atomicAdd(a.list, (uint32_t)__builtin_popcountll(undec));
+            k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
+            if ((undec >> me) & 1ull)
+                a.list[1 + k0 + (uint32_t)__builtin_popcountll(undec & ((1ull << me) - 1ull))] = (uint32_t)(base + me);
+            uint32_t k = k0;
+            for (uint64_t m = undec; m; m &= m - 1ull, ++k) {
+                const uint32_t p = (uint32_t)__builtin_ctzll(m);
+                const uint8_t* s = a.in + (base + p) * 81;
+                uint8_t* d = a.list_in + (uint64_t)k * 81;
+                d[threadIdx.x] = s[threadIdx.x];
+                if (threadIdx.x < 17u) d[64 + threadIdx.x] = s[64 + threadIdx.x];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+#endif
+
+}  // namespace sdk

@@ -1878,6 +1878,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         grid = (uint32_t)min<uint64_t>(gridDim.x, (nb + 3) / 4 + 64ull +
                                                       (uint64_t)ld_agent(&dn->helpers) * min<uint64_t>(nb, kDnHelpCap));
         if (n + resumed == 0 || blockIdx.x >= grid) return;
+    } else if (args.n_dev) {
+        // a prop32 fallback batch: its length is the list the propagation pass left
+        n = min<uint64_t>(*args.n_dev, args.n);
+        if (n == 0) return;
     }
     __shared__ uint2 s_region[2 * kRegion4];
     __shared__ uint8_t s_in[2 * 2 * 81];

@@ -22,6 +22,7 @@
 #include "frontier_kernel.h"
 #include "solve2_kernel.h"   // constants only: the kernel lives in solve2_launch.hip
 #include "solve4_kernel.h"   // constants only: the kernel lives in solve4_launch.hip
+#include "prop32_kernel.h"   // constants only: the kernel lives in prop32_launch.hip
 #define SDK_DEFINE_LANE_KERNEL
 #include "solve_lane_kernel.h"
 
@@ -29,6 +30,7 @@ namespace sdk {
 hipError_t launch_solve2(const SolveArgs& a, unsigned grid, hipStream_t stream);
 hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream);
 int solve4_dn_blocks_per_cu();   // resident workgroups per CU of solve4_kernel<true>
+hipError_t launch_prop32(const Prop32Args& a, unsigned grid, hipStream_t stream);
 hipError_t launch_expand4(const ExpandArgs& a, unsigned grid, hipStream_t stream);   // expand4_kernel.h
 }
 
@@ -315,6 +317,11 @@ struct sdk_ctx {
     int64_t dn_max = 1 << 19;      // largest batch solved in phases (SDK_OPT_DONATE_MAX, 0 = any)
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
     int dn_blocks_per_cu = 0;      // resident solve4_kernel<true> workgroups per CU (queried once)
+    int prop32 = 1;                // QUAD: bit-sliced root propagation first (SDK_OPT_PROP32)
+    int prop32_lc = 4;             // ... a locked-candidates pass every this many steps
+    int64_t prop32_min = 4096;     // ... for batches of at least this many boards
+    bool prop32_ran = false;       // the last solve ran it (p32_list[0] = its undecided boards)
+    DevBuf p32_ctl, p32_list, p32_in, p32_out, p32_st;
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
     DevBuf fr_tail;                // refine_head: the boards kept after the refined ones
     // the device-resident frontier of the last sdk_frontier_build (in fr_a)
@@ -528,7 +535,7 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     a.locked = c->locked;
     a.heads = nullptr;
     a.donate = nullptr;
-    a.n_dev = nullptr;
+    a.n_dev = n_dev;   // the plain and split launches of a prop32 fallback: the list's length
     a.save = nullptr;
     a.save_idx = nullptr;
     // a first-solution scan (frontier_first): the plain QUAD launch cancels boards above the lowest hit
@@ -708,13 +715,27 @@ int dn_prep(sdk_ctx* c, uint64_t cap, bool first_pass) {
     return SDK_OK;
 }
 
+int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t* d_status, size_t n, int order,
+                        int64_t budget, int64_t donate);
+
 int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_t* d_out, int8_t* d_status,
                  uint64_t* d_work, size_t n, int count_mode, uint64_t limit, unsigned long long* d_count,
                  unsigned long long* d_counts = nullptr, uint64_t in_first = 0, uint64_t in_step = 1,
-                 int order = -1, int64_t budget = -1, int64_t donate = -1) {
-    // donate: SDK_OPT_DONATE for this call (-1 = the context's)
+                 int order = -1, int64_t budget = -1, int64_t donate = -1, const uint32_t* n_dev = nullptr) {
+    // donate: SDK_OPT_DONATE for this call (-1 = the context's); n_dev: the batch's length on the
+    // device (n bounds it; the prop32 fallback)
     const int eff_order = order >= 0 ? order : c->order;
     const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
+    if (!n_dev) c->prop32_ran = false;
+    // the bit-sliced root propagation pass first (prop32_kernel.h): plain solves of whole batches
+    // (no first-cell masks, work counters, strided inputs or first-solution scans), 16-byte
+    // aligned, at least prop32_min boards; a budget of 1 node is left to solve4 (a board solved at
+    // its root takes one)
+    if (!n_dev && c->prop32 && c->solver == SDK_SOLVER_QUAD && !count_mode && d_out && d_status && !d_work &&
+        !d_mask && in_first == 0 && in_step <= 1 && !c->first_found && (node_budget == 0 || node_budget >= 2) &&
+        (int64_t)n >= c->prop32_min && n <= kDnCapBoards &&
+        ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15u) == 0)
+        return launch_prop32_solve(c, d_in, d_out, d_status, n, order, budget, donate);
     const int64_t dn = donate >= 0 ? donate : (int64_t)c->donate;
     const uint64_t split = dn == 1 ? kDnSplitDefault : (uint64_t)dn;
     const bool two_phase = n > 0 && !count_mode && dn && c->solver == SDK_SOLVER_QUAD &&
@@ -730,7 +751,8 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     c->dn_resume_now = two_phase && c->dn_resume && c->dn_exhaustive && eff_order == SDK_ORDER_MRV_UNIQUE;
     if (!two_phase)
         return launch_solve_once(c, d_in, d_mask, d_out, d_status, d_work, n, count_mode, limit, d_count, d_counts,
-                                 in_first, in_step, order, budget, 0);
+                                 in_first, in_step, order, budget, 0, n_dev);
+    if (n_dev && n > kDnCapBoards) return fail(SDK_EINVAL, "a device-counted batch is solved in one pass");
     // SDK_OPT_TIMING: the phases of one solve are one timed span
     hipEvent_t stop;
     int rc = timer_begin(c, &stop);
@@ -746,13 +768,59 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
         const uint64_t first = in_first + b0 * step;
         (void)((rc = dn_prep(c, m, b0 == 0)) ||
                (rc = launch_solve_once(c, d_in, mask, out, st, work, m, 0, 0, nullptr, nullptr, first, step, order,
-                                       (int64_t)split, 1)) ||
-               (rc = dn_collect(c, st, m, nullptr, (int8_t)-2, c->dn_list, 0, d_in, mask, first, step, c->dn_in,
+                                       (int64_t)split, 1, n_dev)) ||
+               (rc = dn_collect(c, st, m, n_dev, (int8_t)-2, c->dn_list, 0, d_in, mask, first, step, c->dn_in,
                                 c->dn_mask, c->dn_resume_now)) ||
                (rc = dn_resolve(c, m, c->dn_list, 0, mask != nullptr, out, st, work,
                                 c->dn_exhaustive ? SDK_ORDER_MRV_UNIQUE : SDK_ORDER_LEX, (int64_t)node_budget, c->dn_in,
                                 c->dn_mask, c->dn_out, c->dn_st, c->dn_work,
                                 c->dn_resume_now ? static_cast<uint32_t*>(c->dn_seeds.p) + 1 : nullptr)));
+    }
+    c->timer_hold = false;
+    if (rc) return rc;
+    return timer_end(c, stop);
+}
+
+// The prop32 pass (prop32_kernel.h) over the batch, then the boards it leaves undecided -- listed
+// with their inputs on the device -- solved by the usual path (solve4, phased with donation when
+// that applies) with the list's length read on the device, and their answers scattered back.
+// Every launch is enqueued at once; an empty list costs the fallback's launches a few microseconds.
+int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t* d_status, size_t n, int order,
+                        int64_t budget, int64_t donate) {
+    int rc;
+    constexpr size_t kCtlBytes = (size_t)sdk::kP32Heads * sdk::kP32HeadStride * 4;
+    if ((rc = ensure(c->p32_ctl, kCtlBytes)) || (rc = ensure(c->p32_list, (n + 1) * 4)) ||
+        (rc = ensure(c->p32_in, n * 81)) || (rc = ensure(c->p32_out, n * 81)) || (rc = ensure(c->p32_st, n)))
+        return rc;
+    hipEvent_t stop;
+    if ((rc = timer_begin(c, &stop))) return rc;
+    c->timer_hold = true;   // the pass and its fallback are one timed span
+    HIPCALL(hipMemsetAsync(c->p32_ctl.p, 0, kCtlBytes, c->stream));
+    HIPCALL(hipMemsetAsync(c->p32_list.p, 0, 4, c->stream));
+    sdk::Prop32Args a{};
+    a.in = d_in;
+    a.out = d_out;
+    a.status = d_status;
+    a.n = n;
+    a.heads = static_cast<uint32_t*>(c->p32_ctl.p);
+    a.list = static_cast<uint32_t*>(c->p32_list.p);
+    a.list_in = static_cast<uint8_t*>(c->p32_in.p);
+    a.lc_every = (uint32_t)std::max(1, c->prop32_lc);
+    a.max_steps = 96;
+    const uint64_t groups = (n + 63) / 64;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)c->cus * 20));
+    HIPCALL(sdk::launch_prop32(a, grid, c->stream));
+    c->prop32_ran = true;
+    const uint32_t* lst = static_cast<const uint32_t*>(c->p32_list.p);
+    rc = launch_solve(c, static_cast<uint8_t*>(c->p32_in.p), nullptr, static_cast<uint8_t*>(c->p32_out.p),
+                      static_cast<int8_t*>(c->p32_st.p), nullptr, n, 0, 0, nullptr, nullptr, 0, 1, order, budget,
+                      donate, lst);
+    if (!rc) {
+        const unsigned g = (unsigned)std::min<uint64_t>(n, (uint64_t)c->cus * 16);
+        sdk::dn_scatter_kernel<<<g, 128, 0, c->stream>>>(lst, static_cast<uint8_t*>(c->p32_out.p),
+                                                         static_cast<int8_t*>(c->p32_st.p), nullptr, false, d_out,
+                                                         d_status, nullptr);
+        if (hipGetLastError() != hipSuccess) rc = fail(SDK_EHIP, "prop32 scatter launch failed");
     }
     c->timer_hold = false;
     if (rc) return rc;
@@ -1199,6 +1267,18 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 0 || value > (1 << 30)) return fail(SDK_EINVAL, "donate must be 0, 1 or a split budget >= 2");
             c->donate = (int)value;
             return SDK_OK;
+        case SDK_OPT_PROP32:
+            if (value != 0 && value != 1) return fail(SDK_EINVAL, "SDK_OPT_PROP32 is 0 or 1");
+            c->prop32 = (int)value;
+            return SDK_OK;
+        case SDK_OPT_PROP32_LC:
+            if (value < 1 || value > 64) return fail(SDK_EINVAL, "SDK_OPT_PROP32_LC out of range 1..64");
+            c->prop32_lc = (int)value;
+            return SDK_OK;
+        case SDK_OPT_PROP32_MIN:
+            if (value < 1) return fail(SDK_EINVAL, "SDK_OPT_PROP32_MIN must be >= 1");
+            c->prop32_min = value;
+            return SDK_OK;
         case SDK_OPT_XCD_HEADS:
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "xcd heads must be 0 or 1");
             c->xcd_heads = (int)value;
@@ -1280,6 +1360,19 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_TIMING: *value = c->timing ? 1 : 0; return SDK_OK;
         case SDK_OPT_LOCKED: *value = c->locked; return SDK_OK;
         case SDK_OPT_XCD_HEADS: *value = c->xcd_heads; return SDK_OK;
+        case SDK_OPT_PROP32: *value = c->prop32; return SDK_OK;
+        case SDK_OPT_PROP32_LC: *value = c->prop32_lc; return SDK_OK;
+        case SDK_OPT_PROP32_MIN: *value = c->prop32_min; return SDK_OK;
+        case SDK_OPT_PROP32_UNDECIDED: {
+            *value = 0;
+            if (!c->prop32_ran) return SDK_OK;
+            HIPCALL(hipSetDevice(c->device));
+            uint32_t v = 0;
+            HIPCALL(hipMemcpyAsync(&v, c->p32_list.p, sizeof v, hipMemcpyDeviceToHost, c->stream));
+            HIPCALL(hipStreamSynchronize(c->stream));
+            *value = v;
+            return SDK_OK;
+        }
         case SDK_OPT_DONATE: *value = c->donate; return SDK_OK;
         case SDK_OPT_SPLIT_BOARDS: return read_dn_stat(c, 0, value);
         case SDK_OPT_DONATE_MODE: *value = c->dn_exhaustive; return SDK_OK;

@@ -159,7 +159,8 @@ class SudokuEngine:
     _FORK_OPTIONS = (L.SDK_OPT_ORDER, L.SDK_OPT_NODE_BUDGET, L.SDK_OPT_WAVES_PER_CU, L.SDK_OPT_WORK_COUNTER,
                      L.SDK_OPT_SOLVER, L.SDK_OPT_WAVES_PER_CU2, L.SDK_OPT_SOLVE_CHUNK, L.SDK_OPT_LOCKED,
                      L.SDK_OPT_XCD_HEADS, L.SDK_OPT_DONATE, L.SDK_OPT_DONATE_MODE, L.SDK_OPT_DONATE_MAX,
-                     L.SDK_OPT_DONATE_HELPERS, L.SDK_OPT_DONATE_RESUME)
+                     L.SDK_OPT_DONATE_HELPERS, L.SDK_OPT_DONATE_RESUME, L.SDK_OPT_PROP32, L.SDK_OPT_PROP32_LC,
+                     L.SDK_OPT_PROP32_MIN)
 
     def fork(self):
         """A second engine on the same device with its own context and stream (same options):

@@ -116,6 +116,16 @@ extern "C" {
                                  /* split phase leaves its DFS stack); 0: it restarts    */
 #define SDK_OPT_RESUMED      24  /* read-only: boards of the last phased solve resumed   */
                                  /* from their saved stacks (its last pass; waits)       */
+#define SDK_OPT_PROP32       25  /* QUAD solver: 1 (default) = a batch is first run      */
+                                 /* through bit-sliced root propagation (32 boards per   */
+                                 /* half-wave: singles + locked candidates); boards it   */
+                                 /* does not decide are searched by solve4 and scattered */
+                                 /* back -- same answers and statuses.  Plain solves     */
+                                 /* only (no masks, work counters or strided inputs)     */
+#define SDK_OPT_PROP32_LC    26  /* ... a locked-candidates pass every N steps (default 4) */
+#define SDK_OPT_PROP32_MIN   27  /* ... for batches of at least N boards (default 4096)   */
+#define SDK_OPT_PROP32_UNDECIDED 28 /* read-only: boards the last solve's propagation pass */
+                                 /* left to the search (waits)                           */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

@@ -685,6 +685,20 @@ def launch_ranks(args):
     return max(codes, key=abs)
 
 
+def timer_spans(e):
+    """The context's timed spans since timer_reset, ms each (sdk_debug_timer_list; an engine without
+    the library -- the CPU tests' stub -- reports its total as equal spans)."""
+    if not hasattr(e, "lib"):
+        ms, nl = e.timer_read()
+        return [ms / max(nl, 1)] * nl
+    cap = 1 << 16
+    arr = (ctypes.c_double * cap)()
+    cnt = ctypes.c_int64()
+    if e.lib.sdk_debug_timer_list(e.ctx, arr, ctypes.c_int64(cap), ctypes.byref(cnt)) != 0:
+        raise RuntimeError("sdk_debug_timer_list failed")
+    return list(arr[:min(cnt.value, cap)])
+
+
 def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=True):
     """Time `steps` sdk_solve_batch_dev passes over this rank's resident slice (barrier +
     device sync on both sides, max over ranks); verify every board afterwards.  Each rank's clock
@@ -699,6 +713,7 @@ def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=
     them.  Every pass solves the whole slice; every output buffer is checked.  (The headline uses
     one context: its per-launch HIP events are then the kernel's own duration, the roofline's
     denominator; overlapped launches' events also hold their wait for the GPU.)"""
+    from distributed_sudoku_solver_amd import _lib as L
     n = len(puzzles)
     nctx = max(1, min(int(contexts), max(1, steps)))
     engines = [eng] + [eng.fork() for _ in range(nctx - 1)]
@@ -724,12 +739,18 @@ def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=
     elapsed = time.perf_counter() - t0
     d.barrier()
     kernel_ms, launches = 0.0, 0
+    fallback = []
     for e in engines:
         if timed:
-            ms, nl = e.timer_read()
+            spans = timer_spans(e)
             e.timer_stop()
-            kernel_ms += ms
-            launches += nl
+            if len(spans) == 2 * steps and e.get_option(L.SDK_OPT_PROP32):
+                # a prop32 solve is two spans: the propagation pass (the roofline's kernel) and its
+                # fallback (search of the undecided boards + scatter)
+                fallback += spans[1::2]
+                spans = spans[0::2]
+            kernel_ms += sum(spans)
+            launches += len(spans)
     elapsed_max = d.max(elapsed)
     bad = 0
     out = np.empty((n, 81), np.uint8)
@@ -746,6 +767,7 @@ def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=
     for e in engines[1:]:
         e.close()
     avg_kernel_s = kernel_ms / 1000.0 / max(launches, 1)
+    solve_leg.fallback_ms = sum(fallback) / len(fallback) if fallback else None
     return elapsed_max, avg_kernel_s, bad_total
 
 
@@ -774,6 +796,9 @@ def main():
     if args.waves_per_cu:
         eng.set_option(SOLVERS[args.solver][2], args.waves_per_cu)
     solve_kernel = SOLVERS[args.solver][1]
+    if args.solver == "quad" and eng.get_option(L.SDK_OPT_PROP32):
+        # the QUAD solve's first pass, which decides every C4 board (prop32_kernel.h)
+        solve_kernel = "sdk::prop32_kernel"
     args.solve_kernel = solve_kernel
 
     # -------------------------------------------------------------- checker
@@ -842,6 +867,7 @@ def main():
     s_el, avg_kernel_s, bad_total = solve_leg(eng, d, args, puzzles, expected, args.steps, args.warmup)
     single_stream = {"value": total * args.steps / s_el, "unit": "puzzles/s", "ms_per_step": s_el / args.steps * 1e3,
                      "avg_kernel_ms": avg_kernel_s * 1e3, "contexts": 1,
+                     "avg_fallback_ms": solve_leg.fallback_ms,
                      "parity": {"mismatched_boards": bad_total, "checked_boards": total}}
     inflight = max(1, args.inflight)
     if inflight > 1:

@@ -27,8 +27,8 @@
 //             (T_d, once_d) pairs;
 //   cells:    each cell loses the T of its three units unless closed, takes a hidden single
 //             (a remaining candidate in some unit's once), and "changed" is accumulated.
-// Every lc_every-th step (and whenever every live board is at a fixpoint) the unit/cell phases
-// are replaced by one locked-candidates pass over the 54 box-line triads:
+// After every lc_every-th step the next step's unit/cell phases are replaced by one
+// locked-candidates pass over the 54 box-line triads:
 //   presence P(triad) = OR of its three cells' words (closed cells included, so the pass is sound at
 //   any state); claim(L,B) = P(L,B) & ~P(L,B1) & ~P(L,B2); point(L,B) = P(L,B) & ~P(L1,B) & ~P(L2,B);
 //   a triad's open cells lose claim(L1,B) | claim(L2,B) | point(L,B1) | point(L,B2).
@@ -146,13 +146,76 @@ __device__ __forceinline__ void p32_singles(const P32Lane& w, P32Cells& x, uint3
     }
 }
 
-// the unit summary of the lane's unit (rows 0-8, columns 9-17, boxes 18-26); FIRST (a group's
-// first step: closed cells are the givens) also reports digits given twice (dup: not exact)
-template <bool FIRST>
-__device__ __forceinline__ void p32_unit(const P32Lane& w, uint32_t& miss, uint32_t& dup) {
-    const uint32_t j = p32_opq(w.hl);
-    // cell q of the unit at u0 + (q % 3) ua + (q / 3) ub
-    uint32_t u0, ua, ub;
+// Exact instruction sequences for the step's bit algebra (v_bitop3_b32 truth tables over S0 = 0xF0,
+// S1 = 0xCC, S2 = 0xAA): left to itself the compiler splits the majority and the and-or forms into
+// 3-instruction chains (7 instead of 5 per pair and digit in the unit summary).
+//   unit, first three cells:  ones = a | b | c, twos = maj(a, b, c) (0xE8), T = a&sa | b&sb | c&sc
+//   unit, a pair:             twos |= maj(ones, a, b), ones |= a | b, T |= a&sa | b&sb (0xF8: S0 | S1&S2)
+__device__ __forceinline__ void p32_unit3(uint32_t& ones, uint32_t& twos, uint32_t& T, uint32_t a, uint32_t b,
+                                          uint32_t c, uint32_t sa, uint32_t sb, uint32_t sc) {
+    asm("v_or3_b32 %[o], %[a], %[b], %[c]\n\t"
+        "v_bitop3_b32 %[w], %[a], %[b], %[c] bitop3:0xe8\n\t"
+        "v_and_b32 %[t], %[a], %[sa]\n\t"
+        "v_bitop3_b32 %[t], %[t], %[b], %[sb] bitop3:0xf8\n\t"
+        "v_bitop3_b32 %[t], %[t], %[c], %[sc] bitop3:0xf8"
+        : [o] "=&v"(ones), [w] "=&v"(twos), [t] "=&v"(T)
+        : [a] "v"(a), [b] "v"(b), [c] "v"(c), [sa] "v"(sa), [sb] "v"(sb), [sc] "v"(sc));
+}
+__device__ __forceinline__ void p32_unit2(uint32_t& ones, uint32_t& twos, uint32_t& T, uint32_t a, uint32_t b,
+                                          uint32_t sa, uint32_t sb) {
+    uint32_t t;
+    asm("v_bitop3_b32 %[t], %[o], %[a], %[b] bitop3:0xe8\n\t"
+        "v_or3_b32 %[o], %[o], %[a], %[b]\n\t"
+        "v_or_b32 %[w], %[w], %[t]\n\t"
+        "v_bitop3_b32 %[T], %[T], %[a], %[sa] bitop3:0xf8\n\t"
+        "v_bitop3_b32 %[T], %[T], %[b], %[sb] bitop3:0xf8"
+        : [t] "=&v"(t), [o] "+v"(ones), [w] "+v"(twos), [T] "+v"(T)
+        : [a] "v"(a), [b] "v"(b), [sa] "v"(sa), [sb] "v"(sb));
+}
+// cell update, first pass for digit d:  U = cT|rT|bT, H = cH|rH|bH, c &= ~U | s (0xB0: S0 & (~S1 | S2)),
+// anyh |= c & H (0xF8); with CHG, chg |= c_old & ~c_new (0xF4: S0 | S1 & ~S2)
+template <bool CHG>
+__device__ __forceinline__ void p32_upd1(uint32_t& c, uint32_t& H, uint32_t& anyh, uint32_t& chg, uint32_t s,
+                                         uint32_t cT, uint32_t rT, uint32_t bT, uint32_t cH, uint32_t rH, uint32_t bH) {
+    uint32_t U, v;
+    if (CHG)
+        asm("v_or3_b32 %[u], %[ct], %[rt], %[bt]\n\t"
+            "v_or3_b32 %[h], %[ch], %[rh], %[bh]\n\t"
+            "v_bitop3_b32 %[v], %[c], %[u], %[s] bitop3:0xb0\n\t"
+            "v_bitop3_b32 %[g], %[g], %[c], %[v] bitop3:0xf4\n\t"
+            "v_bitop3_b32 %[a], %[a], %[v], %[h] bitop3:0xf8"
+            : [u] "=&v"(U), [h] "=&v"(H), [v] "=&v"(v), [g] "+v"(chg), [a] "+v"(anyh)
+            : [c] "v"(c), [s] "v"(s), [ct] "v"(cT), [rt] "v"(rT), [bt] "v"(bT), [ch] "v"(cH), [rh] "v"(rH),
+              [bh] "v"(bH));
+    else
+        asm("v_or3_b32 %[u], %[ct], %[rt], %[bt]\n\t"
+            "v_or3_b32 %[h], %[ch], %[rh], %[bh]\n\t"
+            "v_bitop3_b32 %[v], %[c], %[u], %[s] bitop3:0xb0\n\t"
+            "v_bitop3_b32 %[a], %[a], %[v], %[h] bitop3:0xf8"
+            : [u] "=&v"(U), [h] "=&v"(H), [v] "=&v"(v), [a] "+v"(anyh)
+            : [c] "v"(c), [s] "v"(s), [ct] "v"(cT), [rt] "v"(rT), [bt] "v"(bT), [ch] "v"(cH), [rh] "v"(rH),
+              [bh] "v"(bH));
+    c = v;
+}
+// second pass: the hidden single, c &= H | ~anyh (0xD0: S0 & (S1 | ~S2)); with CHG the change bits
+template <bool CHG>
+__device__ __forceinline__ void p32_upd2(uint32_t& c, uint32_t H, uint32_t anyh, uint32_t& chg) {
+    uint32_t v;
+    if (CHG)
+        asm("v_bitop3_b32 %[v], %[c], %[h], %[a] bitop3:0xd0\n\t"
+            "v_bitop3_b32 %[g], %[g], %[c], %[v] bitop3:0xf4"
+            : [v] "=&v"(v), [g] "+v"(chg)
+            : [c] "v"(c), [h] "v"(H), [a] "v"(anyh));
+    else
+        asm("v_bitop3_b32 %[v], %[c], %[h], %[a] bitop3:0xd0" : [v] "=v"(v) : [c] "v"(c), [h] "v"(H), [a] "v"(anyh));
+    c = v;
+}
+
+// the unit summary of the lane's unit (rows 0-8, columns 9-17, boxes 18-26).
+// "In two or more cells" is accumulated two cells at a time after the first three: a bit is in at
+// least two of (ones, a, b) exactly when it is in their majority (bitop3 0xE8), as in solve4's unit4.
+// cell q of the lane's unit at u0 + (q % 3) ua + (q / 3) ub
+__device__ __forceinline__ void p32_unit_cells(uint32_t j, uint32_t& u0, uint32_t& ua, uint32_t& ub) {
     if (j < 9) {                           // row j: cells 9j + q
         u0 = kP32Rec * 9 * j; ua = kP32Rec; ub = 3 * kP32Rec;
     } else if (j < 18) {                   // column j - 9: cells 9q + (j - 9)
@@ -163,37 +226,137 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, uint32_t& miss, uint3
     } else {                               // spare lane: one unwritten record, nine times
         u0 = kP32Rec * (54 + j); ua = 0; ub = 0;
     }
-    uint32_t ones[9], twos[9], T[9];
-    dup = 0u;
+}
+
+// digits given twice in the lane's unit (a group's first step, before p32_unit: its closed cells are
+// the givens); such a board is not exact and goes to the search
+__device__ __forceinline__ uint32_t p32_dups(const P32Lane& w) {
+    uint32_t u0, ua, ub;
+    p32_unit_cells(p32_opq(w.hl), u0, ua, ub);
+    uint32_t T[9], dup = 0u;
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
         const uint32_t o = u0 + (uint32_t)(q % 3) * ua + (uint32_t)(q / 3) * ub;
         const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
                     r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
         const uint32_t a[9] = {r0.x, r0.y, r1.x, r1.y, r2.x, r2.y, r3.x, r3.y, r4.x};
-        const uint32_t s = r4.y;
 #pragma unroll
         for (int d = 0; d < 9; ++d) {
+            const uint32_t t = a[d] & r4.y;
             if (q == 0) {
-                ones[d] = a[d];
-                twos[d] = 0u;
-                T[d] = a[d] & s;
+                T[d] = t;
             } else {
-                if (FIRST) dup |= T[d] & a[d] & s;
-                twos[d] |= ones[d] & a[d];
-                ones[d] |= a[d];
-                T[d] |= a[d] & s;
+                dup |= T[d] & t;
+                T[d] |= t;
             }
         }
-        // one cell's reads at a time: the accumulators pass through here, so the next cell's loads
-        // cannot be hoisted above this cell's arithmetic (left alone the scheduler issues all 45
-        // loads first and spills)
+        // one cell's loads at a time (see p32_unit)
+        asm volatile("" : "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]), "+v"(T[6]),
+                     "+v"(T[7]), "+v"(T[8]), "+v"(dup)::"memory");
+    }
+    return dup;
+}
+
+__device__ __forceinline__ void p32_unit(const P32Lane& w, uint32_t& miss) {
+    const uint32_t j = p32_opq(w.hl);
+    uint32_t u0, ua, ub;
+    p32_unit_cells(j, u0, ua, ub);
+    uint32_t ones[9], twos[9], T[9];
+#if SDK_PROP32_UNIT_PAIR
+    // cells 0, 1 (ten fewer registers than three at a time), then pairs (2, 3) .. (6, 7), then cell 8
+    {
+        uint32_t a[2][9], s[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t o = u0 + (uint32_t)q * ua;
+            const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
+                        r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
+            a[q][0] = r0.x; a[q][1] = r0.y; a[q][2] = r1.x; a[q][3] = r1.y; a[q][4] = r2.x;
+            a[q][5] = r2.y; a[q][6] = r3.x; a[q][7] = r3.y; a[q][8] = r4.x;
+            s[q] = r4.y;
+        }
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            ones[d] = a[0][d] | a[1][d];
+            twos[d] = a[0][d] & a[1][d];
+            T[d] = (a[0][d] & s[0]) | (a[1][d] & s[1]);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
         asm volatile("" : "+v"(ones[0]), "+v"(ones[1]), "+v"(ones[2]), "+v"(ones[3]), "+v"(ones[4]), "+v"(ones[5]),
                      "+v"(ones[6]), "+v"(ones[7]), "+v"(ones[8]), "+v"(twos[0]), "+v"(twos[1]), "+v"(twos[2]),
                      "+v"(twos[3]), "+v"(twos[4]), "+v"(twos[5]), "+v"(twos[6]), "+v"(twos[7]), "+v"(twos[8]),
                      "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]), "+v"(T[6]),
                      "+v"(T[7]), "+v"(T[8])::"memory");
+        const int nq = p < 3 ? 2 : 1;
+        uint32_t a[2][9], s[2];
+#pragma unroll
+        for (int h = 0; h < nq; ++h) {
+            const int q = 2 + 2 * p + h;
+            const uint32_t o = u0 + (uint32_t)(q % 3) * ua + (uint32_t)(q / 3) * ub;
+            const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
+                        r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
+            a[h][0] = r0.x; a[h][1] = r0.y; a[h][2] = r1.x; a[h][3] = r1.y; a[h][4] = r2.x;
+            a[h][5] = r2.y; a[h][6] = r3.x; a[h][7] = r3.y; a[h][8] = r4.x;
+            s[h] = r4.y;
+        }
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            if (nq == 2) {
+                p32_unit2(ones[d], twos[d], T[d], a[0][d], a[1][d], s[0], s[1]);
+            } else {
+                twos[d] |= ones[d] & a[0][d];
+                ones[d] |= a[0][d];
+                T[d] |= a[0][d] & s[0];
+            }
+        }
     }
+#else
+    // cells 0, 1, 2
+    {
+        uint32_t a[3][9], s[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const uint32_t o = u0 + (uint32_t)q * ua;
+            const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
+                        r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
+            a[q][0] = r0.x; a[q][1] = r0.y; a[q][2] = r1.x; a[q][3] = r1.y; a[q][4] = r2.x;
+            a[q][5] = r2.y; a[q][6] = r3.x; a[q][7] = r3.y; a[q][8] = r4.x;
+            s[q] = r4.y;
+        }
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            p32_unit3(ones[d], twos[d], T[d], a[0][d], a[1][d], a[2][d], s[0], s[1], s[2]);
+        }
+    }
+    // cells (3, 4), (5, 6), (7, 8): one pair's reads at a time -- the accumulators pass through the
+    // empty asm after each pair, so the next pair's loads are not hoisted above this pair's
+    // arithmetic (left alone the scheduler issues every load first and spills)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        asm volatile("" : "+v"(ones[0]), "+v"(ones[1]), "+v"(ones[2]), "+v"(ones[3]), "+v"(ones[4]), "+v"(ones[5]),
+                     "+v"(ones[6]), "+v"(ones[7]), "+v"(ones[8]), "+v"(twos[0]), "+v"(twos[1]), "+v"(twos[2]),
+                     "+v"(twos[3]), "+v"(twos[4]), "+v"(twos[5]), "+v"(twos[6]), "+v"(twos[7]), "+v"(twos[8]),
+                     "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]), "+v"(T[6]),
+                     "+v"(T[7]), "+v"(T[8])::"memory");
+        uint32_t a[2][9], s[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = 3 + 2 * p + h;
+            const uint32_t o = u0 + (uint32_t)(q % 3) * ua + (uint32_t)(q / 3) * ub;
+            const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
+                        r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
+            a[h][0] = r0.x; a[h][1] = r0.y; a[h][2] = r1.x; a[h][3] = r1.y; a[h][4] = r2.x;
+            a[h][5] = r2.y; a[h][6] = r3.x; a[h][7] = r3.y; a[h][8] = r4.x;
+            s[h] = r4.y;
+        }
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            p32_unit2(ones[d], twos[d], T[d], a[0][d], a[1][d], s[0], s[1]);
+        }
+    }
+#endif
     miss = 0u;
 #pragma unroll
     for (int d = 0; d < 9; ++d) miss |= ~ones[d];
@@ -203,7 +366,11 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, uint32_t& miss, uint3
     for (int d = 0; d < 9; ++d) p32_st(w.reg, urec + 8 * d, T[d], ones[d] & ~twos[d]);
 }
 
-// the cell update of one step; returns the change bits of the lane's three cells
+__device__ __forceinline__ uint32_t w_rowrec(uint32_t base, int k) { return base + 216u * (uint32_t)k; }
+
+// the cell update of one step; CHG: also returns the change bits of the lane's three cells (only the
+// step before a locked-candidates pass needs them: a board unchanged by it and by the pass is stuck)
+template <bool CHG>
 __device__ __forceinline__ uint32_t p32_cells(const P32Lane& w, P32Cells& x) {
     const uint32_t j = p32_opq(w.hl);
     const uint32_t r0 = j / 9, col = j - 9 * r0;      // cells j + 27k: row r0 + 3k, column col
@@ -221,22 +388,12 @@ __device__ __forceinline__ uint32_t p32_cells(const P32Lane& w, P32Cells& x) {
         uint32_t H[9], anyh = 0u;
 #pragma unroll
         for (int d = 0; d < 9; ++d) {
-            const uint2 r = p32_ld(w.reg, rowrec + 216u * k + 8 * d);   // row r0 + 3k
-            const uint2 b = p32_ld(w.reg, boxrec + 216u * k + 8 * d);   // box 3k + col / 3
-            const uint32_t U = cT[d] | r.x | b.x;
-            H[d] = cH[d] | r.y | b.y;
-            const uint32_t v1 = x.c[k][d] & (~U | x.s[k]);   // a closed cell keeps its digit
-            chg |= x.c[k][d] & ~v1;
-            anyh |= v1 & H[d];
-            x.c[k][d] = v1;
+            const uint2 r = p32_ld(w.reg, w_rowrec(rowrec, k) + 8 * d);   // row r0 + 3k
+            const uint2 b = p32_ld(w.reg, w_rowrec(boxrec, k) + 8 * d);   // box 3k + col / 3
+            p32_upd1<CHG>(x.c[k][d], H[d], anyh, chg, x.s[k], cT[d], r.x, b.x, cH[d], r.y, b.y);
         }
-        // a hidden single: v2 = h | (v1 & ~anyh) = v1 & (H | ~anyh)
 #pragma unroll
-        for (int d = 0; d < 9; ++d) {
-            const uint32_t v2 = x.c[k][d] & (H[d] | ~anyh);
-            chg |= x.c[k][d] & ~v2;
-            x.c[k][d] = v2;
-        }
+        for (int d = 0; d < 9; ++d) p32_upd2<CHG>(x.c[k][d], H[d], anyh, chg);
     }
     return chg;
 }
@@ -362,9 +519,13 @@ __device__ __forceinline__ uint32_t p32_dequeue(const Prop32Args& a, uint32_t gr
     return ~0u;
 }
 
+#ifndef SDK_PROP32_UNIT_PAIR
+#define SDK_PROP32_UNIT_PAIR 0
+#endif
+
 #ifdef SDK_DEFINE_PROP32_KERNEL
 #ifndef SDK_PROP32_WAVES_PER_EU
-#define SDK_PROP32_WAVES_PER_EU 5
+#define SDK_PROP32_WAVES_PER_EU 4
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_WAVES_PER_EU))) void prop32_kernel(
     Prop32Args a) {
@@ -385,14 +546,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         // the group's boards into the staging (row-major, 81 bytes each; half h: boards 32h..)
         const uint8_t* src = a.in + base * 81;
         if (nb == 64) {
+            // 324 pieces of 16 B: 5 per lane, 4 lanes a sixth; piece q of the group to the staging of
+            // half q / 162
+            const uint32_t t = p32_opq(threadIdx.x);
+            p32_u4 v[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+                if (i < 5 || t < 4u) v[i] = reinterpret_cast<const p32_u4*>(src)[t + 64u * i];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                const uint32_t q = threadIdx.x + 64u * i;
-                if (q < 324u) {
-                    const p32_u4 v = reinterpret_cast<const p32_u4*>(src)[q];
-                    const uint32_t o = 16u * q, h = o >= kP32Stage ? 1u : 0u;
-                    *(__attribute__((address_space(3))) p32_u4*)(lds + h * kP32Region + o - h * kP32Stage) = v;
-                }
+                const uint32_t q = t + 64u * i, h = q >= 162u ? 1u : 0u;
+                if (i < 5 || t < 4u)
+                    *(__attribute__((address_space(3))) p32_u4*)(lds + h * (kP32Region - kP32Stage) + 16u * q) = v[i];
             }
         } else {
             for (uint32_t o = threadIdx.x; o < nb * 81u; o += 64u) {
@@ -441,18 +606,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
                 __builtin_amdgcn_wave_barrier();
                 continue;
             }
-            uint32_t miss, dup;
-            if (it == 0)
-                p32_unit<true>(w, miss, dup);
-            else
-                p32_unit<false>(w, miss, dup);
-            const uint64_t badw = p32_mask64(p32_half_or(w.act ? (miss | empty) : 0u));
-            const uint64_t allw = p32_mask64(p32_half_and(w.act ? alls : ~0u));
-            if (it == 0) {
+            if (it == 0) {   // a digit given twice: not exact, to the search
+                const uint32_t dup = p32_dups(w);
                 const uint64_t dupw = p32_mask64(p32_half_or(w.act ? dup : 0u)) & live;
                 undec |= dupw;
                 live &= ~dupw;
             }
+            uint32_t miss;
+            p32_unit(w, miss);
+            const uint64_t badw = p32_mask64(p32_half_or(w.act ? (miss | empty) : 0u));
+            const uint64_t allw = p32_mask64(p32_half_and(w.act ? alls : ~0u));
             const uint64_t sv = allw & ~badw & live, ct = badw & live;
             solved |= sv;
             contra |= ct;
@@ -463,12 +626,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
                 break;
             }
             __builtin_amdgcn_wave_barrier();
-            const uint32_t chg_own = p32_cells(w, x);
-            const uint64_t chgw = p32_mask64(p32_half_or(w.act ? chg_own : 0u));
-            fixw = live & ~chgw;
-            // the next step is a locked-candidates pass every lc_every-th step, and whenever every
-            // live board is at a singles fixpoint
-            lc = (it % a.lc_every) == 0u || fixw == live;
+            // every lc_every-th step is followed by a locked-candidates pass; that step also reports
+            // which boards it left unchanged (a board unchanged by it and by the pass is stuck)
+            lc = (it % a.lc_every) == 0u;
+            if (lc) {
+                const uint32_t chg_own = p32_cells<true>(w, x);
+                fixw = live & ~p32_mask64(p32_half_or(w.act ? chg_own : 0u));
+            } else {
+                (void)p32_cells<false>(w, x);
+            }
             __builtin_amdgcn_wave_barrier();
         }
         __builtin_amdgcn_wave_barrier();
@@ -507,14 +673,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
             // undecided boards' rows get what the staging holds; the search's answers replace them
             uint8_t* dst = a.out + base * 81;
             if (nb == 64) {
+                const uint32_t t = p32_opq(threadIdx.x);
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
-                    const uint32_t q = threadIdx.x + 64u * i;
-                    if (q < 324u) {
-                        const uint32_t o = 16u * q, h = o >= kP32Stage ? 1u : 0u;
+                    const uint32_t q = t + 64u * i, h = q >= 162u ? 1u : 0u;
+                    if (i < 5 || t < 4u)
                         reinterpret_cast<p32_u4*>(dst)[q] =
-                            *(const __attribute__((address_space(3))) p32_u4*)(lds + h * kP32Region + o - h * kP32Stage);
-                    }
+                            *(const __attribute__((address_space(3))) p32_u4*)(lds + h * (kP32Region - kP32Stage) + 16u * q);
                 }
             } else {
                 for (uint32_t o = threadIdx.x; o < nb * 81u; o += 64u) {

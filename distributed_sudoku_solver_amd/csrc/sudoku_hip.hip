@@ -792,11 +792,11 @@ int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t*
     if ((rc = ensure(c->p32_ctl, kCtlBytes)) || (rc = ensure(c->p32_list, (n + 1) * 4)) ||
         (rc = ensure(c->p32_in, n * 81)) || (rc = ensure(c->p32_out, n * 81)) || (rc = ensure(c->p32_st, n)))
         return rc;
-    hipEvent_t stop;
-    if ((rc = timer_begin(c, &stop))) return rc;
-    c->timer_hold = true;   // the pass and its fallback are one timed span
     HIPCALL(hipMemsetAsync(c->p32_ctl.p, 0, kCtlBytes, c->stream));
     HIPCALL(hipMemsetAsync(c->p32_list.p, 0, 4, c->stream));
+    // SDK_OPT_TIMING: two spans, the pass itself and its fallback (search + scatter) as one
+    hipEvent_t stop;
+    if ((rc = timer_begin(c, &stop))) return rc;
     sdk::Prop32Args a{};
     a.in = d_in;
     a.out = d_out;
@@ -810,6 +810,8 @@ int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t*
     const uint64_t groups = (n + 63) / 64;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)c->cus * 20));
     HIPCALL(sdk::launch_prop32(a, grid, c->stream));
+    if ((rc = timer_end(c, stop)) || (rc = timer_begin(c, &stop))) return rc;
+    c->timer_hold = true;
     c->prop32_ran = true;
     const uint32_t* lst = static_cast<const uint32_t*>(c->p32_list.p);
     rc = launch_solve(c, static_cast<uint8_t*>(c->p32_in.p), nullptr, static_cast<uint8_t*>(c->p32_out.p),

@@ -8,5 +8,6 @@ S=distributed_sudoku_solver_amd/csrc
 $H -c -o $out/a.o $S/sudoku_hip.hip &
 $H -mllvm -simplifycfg-sink-common=false -c -o $out/b.o $S/solve2_launch.hip &
 $H -mllvm -simplifycfg-sink-common=false -c -o $out/c.o $S/solve4_launch.hip &
+[ -f $S/prop32_launch.hip ] && $H -fno-slp-vectorize -fno-vectorize -c -o $out/d.o $S/prop32_launch.hip &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/variants/lib_$name.so $out/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

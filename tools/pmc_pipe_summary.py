@@ -102,14 +102,19 @@ def summarize(ctr, wall):
 def main(d):
     out = {}
     units = {"c4": 10_000_000, "hard1m": 1_000_000, "min": 1_048_576}
+    # the kernel each run is summarised for: C4's boards are all decided by the prop32 pass (round 5);
+    # the search workloads' time is solve4's (PMC_C4_KERNEL / PMC_SEARCH_KERNEL override)
+    kern = {"c4": os.environ.get("PMC_C4_KERNEL", "prop32_kernel"),
+            "hard1m": os.environ.get("PMC_SEARCH_KERNEL", "solve4_kernel<false"),
+            "min": os.environ.get("PMC_SEARCH_KERNEL", "solve4_kernel<false")}
     for run in ("c4", "hard1m", "min"):
-        rec = {"units_per_launch": units[run]}
+        rec = {"units_per_launch": units[run], "kernel": kern[run]}
         for part in ("pipe", "lds"):
-            ctr, wall = load(d, f"{run}_{part}")
+            ctr, wall = load(d, f"{run}_{part}", kern[run])
             s = summarize(ctr, wall)
             if s:
                 rec[part] = s
-        if len(rec) > 1:
+        if len(rec) > 2:
             out[run] = rec
     with open(os.path.join(d, "pmc_pipe.json"), "w") as fh:
         json.dump(out, fh, indent=1)

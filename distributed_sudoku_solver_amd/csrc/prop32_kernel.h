@@ -489,6 +489,74 @@ __device__ __forceinline__ uint32_t p32_locked(const P32Lane& w, P32Cells& x) {
     return chg;
 }
 
+// One cell of the half's 32 boards, from the staging (byte of board b at col[81 b]) to its nine
+// candidate words.  Per 8 boards: the 8 bytes as a 64-bit word (byte r = board r), an 8 x 8 bit
+// transpose (three swap stages; Hacker's Delight 7-3) makes byte i the bit-i plane of the 8 boards,
+// v_perm gathers the planes of the 32 boards, and each digit's word is its minterm over the low
+// four planes (values > 9 are the inert boards, decided elsewhere), or'd with the empty cells.
+__device__ __forceinline__ void p32_convert(const p32_lds_t* col, uint32_t (&c)[9]) {
+    uint32_t lo[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        uint32_t l = col[81u * (8 * m)], h = col[81u * (8 * m + 4)];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+            l |= (uint32_t)col[81u * (8 * m + r)] << (8 * r);
+            h |= (uint32_t)col[81u * (8 * m + 4 + r)] << (8 * r);
+        }
+        uint32_t t;
+        t = (l ^ (l >> 7)) & 0x00AA00AAu;  l ^= t ^ (t << 7);
+        t = (h ^ (h >> 7)) & 0x00AA00AAu;  h ^= t ^ (t << 7);
+        t = (l ^ (l >> 14)) & 0x0000CCCCu; l ^= t ^ (t << 14);
+        t = (h ^ (h >> 14)) & 0x0000CCCCu; h ^= t ^ (t << 14);
+        t = (l ^ (h << 4)) & 0xF0F0F0F0u;  l ^= t;       // the high word is not needed after this
+        lo[m] = l;                         // byte i: plane i of boards 8m .. 8m + 7
+    }
+    uint32_t P[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        // bytes (lo[0].i, lo[1].i) and (lo[2].i, lo[3].i); selector 0x0C = a zero byte
+        const uint32_t a = __builtin_amdgcn_perm(lo[1], lo[0], 0x0C0C0400u + 0x0101u * (uint32_t)i);
+        const uint32_t b = __builtin_amdgcn_perm(lo[3], lo[2], 0x04000C0Cu + 0x01010000u * (uint32_t)i);
+        P[i] = a | b;
+    }
+    const uint32_t e = ~(P[0] | P[1] | P[2] | P[3]);        // empty cells: every digit
+    const uint32_t n3 = ~P[3];
+    c[0] = (P[0] & ~P[1] & ~P[2] & n3) | e;                 // 1 = 0001
+    c[1] = (~P[0] & P[1] & ~P[2] & n3) | e;                 // 2 = 0010
+    c[2] = (P[0] & P[1] & ~P[2] & n3) | e;                  // 3 = 0011
+    c[3] = (~P[0] & ~P[1] & P[2] & n3) | e;                 // 4 = 0100
+    c[4] = (P[0] & ~P[1] & P[2] & n3) | e;                  // 5 = 0101
+    c[5] = (~P[0] & P[1] & P[2] & n3) | e;                  // 6 = 0110
+    c[6] = (P[0] & P[1] & P[2] & n3) | e;                   // 7 = 0111
+    c[7] = (P[3] & ~P[0]) | e;                              // 8 = 1000 (9 < v < 16: inert)
+    c[8] = (P[3] & P[0]) | e;                               // 9 = 1001
+}
+
+// The inverse of p32_convert for one cell: the digit of each of the 32 boards (the binary planes of
+// its one-hot words, gathered 8 boards at a time and bit-transposed back into bytes) into the
+// staging, byte of board b at col[81 b].  Only solved boards' digits are meaningful.
+__device__ __forceinline__ void p32_digits(const uint32_t (&c)[9], p32_lds_t* col) {
+    const uint32_t Q[4] = {c[0] | c[2] | c[4] | c[6] | c[8], c[1] | c[2] | c[5] | c[6], c[3] | c[4] | c[5] | c[6],
+                           c[7] | c[8]};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        // byte i: plane i of boards 8m .. 8m + 7 (the high word, planes 4..7, is zero)
+        const uint32_t a = __builtin_amdgcn_perm(Q[1], Q[0], 0x0C0C0400u + 0x0101u * (uint32_t)m);
+        const uint32_t b = __builtin_amdgcn_perm(Q[3], Q[2], 0x04000C0Cu + 0x01010000u * (uint32_t)m);
+        uint32_t l = a | b, t;
+        t = (l ^ (l >> 7)) & 0x00AA00AAu;  l ^= t ^ (t << 7);
+        t = (l ^ (l >> 14)) & 0x0000CCCCu; l ^= t ^ (t << 14);
+        const uint32_t h = (l >> 4) & 0x0F0F0F0Fu;   // boards 8m + 4 .. 8m + 7
+        l &= 0x0F0F0F0Fu;                             // boards 8m .. 8m + 3
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            col[81u * (8 * m + r)] = (uint8_t)(l >> (8 * r));
+            col[81u * (8 * m + 4 + r)] = (uint8_t)(h >> (8 * r));
+        }
+    }
+}
+
 // the 64-bit board mask of a half-reduced word (lane 0: boards 0..31, lane 32: boards 32..63)
 __device__ __forceinline__ uint64_t p32_mask64(uint32_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
@@ -545,20 +613,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         const uint32_t nb = (uint32_t)min<uint64_t>(64, a.n - base);
         // the group's boards into the staging (row-major, 81 bytes each; half h: boards 32h..)
         const uint8_t* src = a.in + base * 81;
+        bool hi_given = true;      // a byte > 9 may be in the group: find the inert boards one by one
         if (nb == 64) {
             // 324 pieces of 16 B: 5 per lane, 4 lanes a sixth; piece q of the group to the staging of
-            // half q / 162
+            // half q / 162.  Every byte is also tested for > 9 (bytewise, exact: the high bit of
+            // (b & 0x7F) + 0x76, or of b itself)
             const uint32_t t = p32_opq(threadIdx.x);
             p32_u4 v[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i)
                 if (i < 5 || t < 4u) v[i] = reinterpret_cast<const p32_u4*>(src)[t + 64u * i];
+            uint32_t hi = 0u;
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const uint32_t q = t + 64u * i, h = q >= 162u ? 1u : 0u;
-                if (i < 5 || t < 4u)
+                if (i < 5 || t < 4u) {
                     *(__attribute__((address_space(3))) p32_u4*)(lds + h * (kP32Region - kP32Stage) + 16u * q) = v[i];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) hi |= ((v[i][e] & 0x7F7F7F7Fu) + 0x76767676u) | v[i][e];
+                }
             }
+            hi_given = __builtin_amdgcn_ballot_w64((hi & 0x80808080u) != 0u) != 0ull;
         } else {
             for (uint32_t o = threadIdx.x; o < nb * 81u; o += 64u) {
                 const uint32_t h = o >= kP32Stage ? 1u : 0u;
@@ -566,28 +641,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
             }
         }
         __builtin_amdgcn_wave_barrier();
-        // bit-sliced candidate words: digit v -> one word, 0 -> all nine, > 9 -> inert (undecided)
-        P32Cells x;
-        uint32_t inert = 0u;
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-#pragma unroll
-            for (int d = 0; d < 9; ++d) x.c[k][d] = 0u;
-#pragma unroll 2
-        for (uint32_t b = 0; b < 32; ++b) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const uint32_t v = w.reg[b * 81u + w.hl + 27u * k];
-                const uint32_t m = v == 0u ? 0x1FFu : (v <= 9u ? 1u << (v - 1u) : 0u);
-                inert |= (v > 9u ? 1u : 0u) << b;
-#pragma unroll
-                for (int d = 0; d < 9; ++d) x.c[k][d] |= ((m >> d) & 1u) << b;
+        // the boards with a given > 9 (inert cells, undecided here): lane L scans board L's row
+        uint64_t inert64 = 0ull;
+        if (hi_given) {
+            bool bad = false;
+            if (threadIdx.x < nb) {
+                const p32_lds_t* row = lds + (threadIdx.x >> 5) * kP32Region + (threadIdx.x & 31u) * 81u;
+                for (uint32_t c = 0; c < 81u; ++c) bad |= row[c] > 9u;
             }
+            inert64 = __builtin_amdgcn_ballot_w64(bad);
         }
+        // bit-sliced candidate words: digit v -> one word, 0 -> all nine (boards with a given > 9 are
+        // undecided; their words do not matter)
+        P32Cells x;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p32_convert(w.reg + w.hl + 27u * k, x.c[k]);
         // per-group bookkeeping as 64-bit board masks in scalar registers (bit 32h + b: board b of
         // half h)
         const uint64_t valid = nb >= 64u ? ~0ull : ((1ull << nb) - 1ull);
-        uint64_t undec = p32_mask64(p32_half_or(w.act ? inert : 0u)) & valid;
+        uint64_t undec = inert64 & valid;
         uint64_t live = valid & ~undec, solved = 0ull, contra = 0ull, fixw = 0ull;
         bool lc = false;
         for (uint32_t it = 0;;) {
@@ -640,26 +712,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         __builtin_amdgcn_wave_barrier();
         // the answers, in the staging: solved boards' digits (binary planes of the one-hot words),
         // boards without a completion their input (DHT_Node.py:535); then out, for the whole group
-        if (solved) {
-            uint32_t p0[3], p1[3], p2[3], p3[3];
+        if (solved && w.act) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                p0[k] = x.c[k][0] | x.c[k][2] | x.c[k][4] | x.c[k][6] | x.c[k][8];
-                p1[k] = x.c[k][1] | x.c[k][2] | x.c[k][5] | x.c[k][6];
-                p2[k] = x.c[k][3] | x.c[k][4] | x.c[k][5] | x.c[k][6];
-                p3[k] = x.c[k][7] | x.c[k][8];
-            }
-            if (w.act) {
-#pragma unroll 2
-                for (uint32_t b = 0; b < 32; ++b) {
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        const uint32_t v = ((p0[k] >> b) & 1u) | (((p1[k] >> b) & 1u) << 1) |
-                                           (((p2[k] >> b) & 1u) << 2) | (((p3[k] >> b) & 1u) << 3);
-                        w.reg[b * 81u + w.hl + 27u * k] = (uint8_t)v;
-                    }
-                }
-            }
+            for (int k = 0; k < 3; ++k) p32_digits(x.c[k], w.reg + w.hl + 27u * k);
         }
         for (uint64_t m = contra; m; m &= m - 1ull) {     // rare: the 81 bytes by 64 lanes
             const uint32_t p = (uint32_t)__builtin_ctzll(m);

@@ -54,6 +54,8 @@ SDK_OPT_PROP32 = 25
 SDK_OPT_PROP32_LC = 26
 SDK_OPT_PROP32_MIN = 27
 SDK_OPT_PROP32_UNDECIDED = 28
+SDK_OPT_PROP32_HANDOVER = 29
+SDK_OPT_PROP32_TAIL = 30
 SDK_DONATE_CONTEXT = -1    # sdk_solve_batch_ex: use the context's SDK_OPT_DONATE
 SDK_CHECK_REG1 = 0
 SDK_CHECK_REG2 = 1

@@ -69,6 +69,11 @@ struct Prop32Args {
     uint8_t* list_in;        // the undecided boards' inputs, dense, in list order
     uint32_t lc_every;       // a locked-candidates pass every lc_every-th step
     uint32_t max_steps;      // boards still live after this many steps are undecided
+    int handover;            // the list gets an undecided board's propagated grid (its closed cells
+                             // filled in: the same completions) instead of its input; not for
+                             // boards with a duplicated or out-of-domain given
+    uint32_t tail_live;      // handover: from step tail_step on, a group with at most this many
+    uint32_t tail_step;      // live boards hands them to the search and ends (0 = never)
 };
 
 // OR / AND over the 32 lanes of each half, result in every lane of the half: rotations inside
@@ -535,10 +540,12 @@ __device__ __forceinline__ void p32_convert(const p32_lds_t* col, uint32_t (&c)[
 
 // The inverse of p32_convert for one cell: the digit of each of the 32 boards (the binary planes of
 // its one-hot words, gathered 8 boards at a time and bit-transposed back into bytes) into the
-// staging, byte of board b at col[81 b].  Only solved boards' digits are meaningful.
-__device__ __forceinline__ void p32_digits(const uint32_t (&c)[9], p32_lds_t* col) {
-    const uint32_t Q[4] = {c[0] | c[2] | c[4] | c[6] | c[8], c[1] | c[2] | c[5] | c[6], c[3] | c[4] | c[5] | c[6],
-                           c[7] | c[8]};
+// staging, byte of board b at col[81 b]; 0 where the cell is open.  (Boards with a contradiction or
+// an inert given get meaningless bytes.)
+__device__ __forceinline__ void p32_digits(const uint32_t (&c)[9], uint32_t single, p32_lds_t* col) {
+    // open cells (more than one candidate left) come out as 0
+    const uint32_t Q[4] = {(c[0] | c[2] | c[4] | c[6] | c[8]) & single, (c[1] | c[2] | c[5] | c[6]) & single,
+                           (c[3] | c[4] | c[5] | c[6]) & single, (c[7] | c[8]) & single};
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         // byte i: plane i of boards 8m .. 8m + 7 (the high word, planes 4..7, is zero)
@@ -591,7 +598,33 @@ __device__ __forceinline__ uint32_t p32_dequeue(const Prop32Args& a, uint32_t gr
 #define SDK_PROP32_UNIT_PAIR 0
 #endif
 
+// SDK_PROP32_STATS (profiling builds only): per group, histograms of the steps it ran, of the step at
+// which at most 4 / at most 1 of its boards were still live, and the locked-candidates passes
+#ifndef SDK_PROP32_STATS
+#define SDK_PROP32_STATS 0
+#endif
+#if SDK_PROP32_STATS
+__device__ unsigned long long g_p32_stats[4][128];
+#define P32_STAT(k, v) atomicAdd(&g_p32_stats[k][min((uint32_t)(v), 127u)], 1ull)
+#else
+#define P32_STAT(k, v) ((void)0)
+#endif
+
 #ifdef SDK_DEFINE_PROP32_KERNEL
+// The fallback's answers back into the batch: listed board i is board list[1 + i]; a board the search
+// did not solve gets its own input back (DHT_Node.py:535), not the propagated grid it was searched from.
+__global__ void p32_scatter_kernel(const uint32_t* list, const uint8_t* sub_out, const int8_t* sub_st,
+                                   const uint8_t* in, uint8_t* out, int8_t* status) {
+    const uint32_t m = list[0];
+    for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
+        const uint64_t j = list[1 + i];
+        const int8_t st = sub_st[i];
+        if (threadIdx.x < 81)
+            out[j * 81 + threadIdx.x] = st == 1 ? sub_out[(uint64_t)i * 81 + threadIdx.x] : in[j * 81 + threadIdx.x];
+        if (threadIdx.x == 0) status[j] = st;
+    }
+}
+
 #ifndef SDK_PROP32_WAVES_PER_EU
 #define SDK_PROP32_WAVES_PER_EU 4
 #endif
@@ -659,14 +692,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         // per-group bookkeeping as 64-bit board masks in scalar registers (bit 32h + b: board b of
         // half h)
         const uint64_t valid = nb >= 64u ? ~0ull : ((1ull << nb) - 1ull);
-        uint64_t undec = inert64 & valid;
+        uint64_t undec = inert64 & valid, inexact = undec;
         uint64_t live = valid & ~undec, solved = 0ull, contra = 0ull, fixw = 0ull;
         bool lc = false;
-        for (uint32_t it = 0;;) {
+#if SDK_PROP32_STATS
+        uint32_t st_lc = 0, st_t4 = ~0u, st_t1 = ~0u;
+#endif
+        uint32_t it = 0;
+        for (;;) {
             uint32_t empty, alls;
             p32_singles(w, x, empty, alls);
             __builtin_amdgcn_wave_barrier();
             if (lc) {
+#if SDK_PROP32_STATS
+                ++st_lc;
+#endif
                 const uint32_t lc_own = p32_locked(w, x);
                 const uint64_t lchg = p32_mask64(p32_half_or(w.act ? lc_own : 0u));
                 const uint64_t stuck = fixw & ~lchg & live;
@@ -682,6 +722,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
                 const uint32_t dup = p32_dups(w);
                 const uint64_t dupw = p32_mask64(p32_half_or(w.act ? dup : 0u)) & live;
                 undec |= dupw;
+                inexact |= dupw;
                 live &= ~dupw;
             }
             uint32_t miss;
@@ -692,7 +733,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
             solved |= sv;
             contra |= ct;
             live &= ~(sv | ct);
+#if SDK_PROP32_STATS
+            if (st_t4 == ~0u && __builtin_popcountll(live) <= 4) st_t4 = it;
+            if (st_t1 == ~0u && __builtin_popcountll(live) <= 1) st_t1 = it;
+#endif
             if (live == 0ull) break;
+            if (a.tail_live && it >= a.tail_step && (uint32_t)__builtin_popcountll(live) <= a.tail_live) {
+                undec |= live;   // the last few boards go to the search with their propagated grids
+                break;
+            }
             if (++it >= a.max_steps) {
                 undec |= live;
                 break;
@@ -709,12 +758,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
             }
             __builtin_amdgcn_wave_barrier();
         }
+#if SDK_PROP32_STATS
+        if (threadIdx.x == 0) {
+            P32_STAT(0, it);
+            P32_STAT(1, st_t4);
+            P32_STAT(2, st_t1);
+            P32_STAT(3, st_lc);
+        }
+#endif
         __builtin_amdgcn_wave_barrier();
         // the answers, in the staging: solved boards' digits (binary planes of the one-hot words),
         // boards without a completion their input (DHT_Node.py:535); then out, for the whole group
-        if (solved && w.act) {
+        uint64_t handed = a.handover ? undec & ~inexact : 0ull;   // listed with their grids
+        if (handed) {
+            // a handed-over grid is searched as a board of its own: two closed cells with one digit
+            // in a unit would be duplicated givens there (whose reference semantics differ), and they
+            // are a contradiction here -- such a board has no completion
+            uint32_t empty, alls;
+            p32_singles(w, x, empty, alls);
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t dupw = p32_mask64(p32_half_or(w.act ? p32_dups(w) : 0u)) & handed;
+            contra |= dupw;
+            undec &= ~dupw;
+            handed &= ~dupw;
+            __builtin_amdgcn_wave_barrier();
+        }
+        if ((solved | handed) && w.act) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) p32_digits(x.c[k], w.reg + w.hl + 27u * k);
+            for (int k = 0; k < 3; ++k) p32_digits(x.c[k], x.s[k], w.reg + w.hl + 27u * k);
         }
         for (uint64_t m = contra; m; m &= m - 1ull) {     // rare: the 81 bytes by 64 lanes
             const uint32_t p = (uint32_t)__builtin_ctzll(m);
@@ -756,10 +827,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
             uint32_t k = k0;
             for (uint64_t m = undec; m; m &= m - 1ull, ++k) {
                 const uint32_t p = (uint32_t)__builtin_ctzll(m);
-                const uint8_t* s = a.in + (base + p) * 81;
                 uint8_t* d = a.list_in + (uint64_t)k * 81;
-                d[threadIdx.x] = s[threadIdx.x];
-                if (threadIdx.x < 17u) d[64 + threadIdx.x] = s[64 + threadIdx.x];
+                if ((handed >> p) & 1ull) {      // the propagated grid, from the staging
+                    const p32_lds_t* s = lds + (p >> 5) * kP32Region + (p & 31u) * 81u;
+                    d[threadIdx.x] = s[threadIdx.x];
+                    if (threadIdx.x < 17u) d[64 + threadIdx.x] = s[64 + threadIdx.x];
+                } else {
+                    const uint8_t* s = a.in + (base + p) * 81;
+                    d[threadIdx.x] = s[threadIdx.x];
+                    if (threadIdx.x < 17u) d[64 + threadIdx.x] = s[64 + threadIdx.x];
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();

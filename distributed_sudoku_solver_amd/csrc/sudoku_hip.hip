@@ -31,6 +31,8 @@ hipError_t launch_solve2(const SolveArgs& a, unsigned grid, hipStream_t stream);
 hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream);
 int solve4_dn_blocks_per_cu();   // resident workgroups per CU of solve4_kernel<true>
 hipError_t launch_prop32(const Prop32Args& a, unsigned grid, hipStream_t stream);
+hipError_t launch_p32_scatter(const uint32_t* list, const uint8_t* sub_out, const int8_t* sub_st, const uint8_t* in,
+                              uint8_t* out, int8_t* status, unsigned grid, hipStream_t stream);
 hipError_t launch_expand4(const ExpandArgs& a, unsigned grid, hipStream_t stream);   // expand4_kernel.h
 }
 
@@ -320,6 +322,9 @@ struct sdk_ctx {
     int prop32 = 1;                // QUAD: bit-sliced root propagation first (SDK_OPT_PROP32)
     int prop32_lc = 4;             // ... a locked-candidates pass every this many steps
     int64_t prop32_min = 4096;     // ... for batches of at least this many boards
+    int prop32_handover = 1;       // ... undecided boards searched from their propagated grids
+    int prop32_tail_live = 0;      // ... a group's last (at most this many) live boards handed over
+    int prop32_tail_step = 24;     //     from this step on (SDK_OPT_PROP32_TAIL = live | step << 8)
     bool prop32_ran = false;       // the last solve ran it (p32_list[0] = its undecided boards)
     DevBuf p32_ctl, p32_list, p32_in, p32_out, p32_st;
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
@@ -807,6 +812,12 @@ int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t*
     a.list_in = static_cast<uint8_t*>(c->p32_in.p);
     a.lc_every = (uint32_t)std::max(1, c->prop32_lc);
     a.max_steps = 96;
+    // the search continues from the propagated grids when no node budget applies (a budget counts
+    // nodes from the input, so the statuses of budget hits would differ)
+    const uint64_t node_budget = budget >= 0 ? (uint64_t)budget : c->budget;
+    a.handover = (c->prop32_handover && node_budget == 0) ? 1 : 0;
+    a.tail_live = a.handover ? (uint32_t)c->prop32_tail_live : 0u;
+    a.tail_step = (uint32_t)c->prop32_tail_step;
     const uint64_t groups = (n + 63) / 64;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)c->cus * 20));
     HIPCALL(sdk::launch_prop32(a, grid, c->stream));
@@ -819,10 +830,9 @@ int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t*
                       donate, lst);
     if (!rc) {
         const unsigned g = (unsigned)std::min<uint64_t>(n, (uint64_t)c->cus * 16);
-        sdk::dn_scatter_kernel<<<g, 128, 0, c->stream>>>(lst, static_cast<uint8_t*>(c->p32_out.p),
-                                                         static_cast<int8_t*>(c->p32_st.p), nullptr, false, d_out,
-                                                         d_status, nullptr);
-        if (hipGetLastError() != hipSuccess) rc = fail(SDK_EHIP, "prop32 scatter launch failed");
+        if (sdk::launch_p32_scatter(lst, static_cast<uint8_t*>(c->p32_out.p), static_cast<int8_t*>(c->p32_st.p), d_in,
+                                    d_out, d_status, g, c->stream) != hipSuccess)
+            rc = fail(SDK_EHIP, "prop32 scatter launch failed");
     }
     c->timer_hold = false;
     if (rc) return rc;
@@ -1281,6 +1291,15 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             if (value < 1) return fail(SDK_EINVAL, "SDK_OPT_PROP32_MIN must be >= 1");
             c->prop32_min = value;
             return SDK_OK;
+        case SDK_OPT_PROP32_HANDOVER:
+            if (value != 0 && value != 1) return fail(SDK_EINVAL, "SDK_OPT_PROP32_HANDOVER is 0 or 1");
+            c->prop32_handover = (int)value;
+            return SDK_OK;
+        case SDK_OPT_PROP32_TAIL:
+            if (value < 0 || (value & 0xFF) > 64 || (value >> 8) > 96) return fail(SDK_EINVAL, "SDK_OPT_PROP32_TAIL out of range");
+            c->prop32_tail_live = (int)(value & 0xFF);
+            c->prop32_tail_step = (int)(value >> 8);
+            return SDK_OK;
         case SDK_OPT_XCD_HEADS:
             if (value != 0 && value != 1) return fail(SDK_EINVAL, "xcd heads must be 0 or 1");
             c->xcd_heads = (int)value;
@@ -1365,6 +1384,8 @@ int sdk_get_option(sdk_ctx* c, int key, int64_t* value) {
         case SDK_OPT_PROP32: *value = c->prop32; return SDK_OK;
         case SDK_OPT_PROP32_LC: *value = c->prop32_lc; return SDK_OK;
         case SDK_OPT_PROP32_MIN: *value = c->prop32_min; return SDK_OK;
+        case SDK_OPT_PROP32_HANDOVER: *value = c->prop32_handover; return SDK_OK;
+        case SDK_OPT_PROP32_TAIL: *value = c->prop32_tail_live | (c->prop32_tail_step << 8); return SDK_OK;
         case SDK_OPT_PROP32_UNDECIDED: {
             *value = 0;
             if (!c->prop32_ran) return SDK_OK;

@@ -160,7 +160,7 @@ class SudokuEngine:
                      L.SDK_OPT_SOLVER, L.SDK_OPT_WAVES_PER_CU2, L.SDK_OPT_SOLVE_CHUNK, L.SDK_OPT_LOCKED,
                      L.SDK_OPT_XCD_HEADS, L.SDK_OPT_DONATE, L.SDK_OPT_DONATE_MODE, L.SDK_OPT_DONATE_MAX,
                      L.SDK_OPT_DONATE_HELPERS, L.SDK_OPT_DONATE_RESUME, L.SDK_OPT_PROP32, L.SDK_OPT_PROP32_LC,
-                     L.SDK_OPT_PROP32_MIN)
+                     L.SDK_OPT_PROP32_MIN, L.SDK_OPT_PROP32_HANDOVER, L.SDK_OPT_PROP32_TAIL)
 
     def fork(self):
         """A second engine on the same device with its own context and stream (same options):

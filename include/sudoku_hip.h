@@ -126,6 +126,12 @@ extern "C" {
 #define SDK_OPT_PROP32_MIN   27  /* ... for batches of at least N boards (default 4096)   */
 #define SDK_OPT_PROP32_UNDECIDED 28 /* read-only: boards the last solve's propagation pass */
                                  /* left to the search (waits)                           */
+#define SDK_OPT_PROP32_HANDOVER 29 /* ... 1 (default): with no node budget the search     */
+                                 /* starts from a board's propagated grid (same          */
+                                 /* completions); 0: from its input                      */
+#define SDK_OPT_PROP32_TAIL  30  /* ... live | step << 8: from `step` on, a 64-board     */
+                                 /* group with at most `live` boards still open hands     */
+                                 /* them to the search (0 = never)                       */
 
 #define SDK_CHECK_REG1       0  /* 1 tile ahead, staged in VGPRs (check_kernel)        */
 #define SDK_CHECK_REG2       1  /* 2 tiles ahead, VGPR ring (check_kernel_rr2)         */

@@ -55,9 +55,11 @@ def edge_boards(n, seed=5):
     return out
 
 
-def run(e, boards, prop, order):
+def run(e, boards, prop, order, opts=()):
     e.set_option(L.SDK_OPT_PROP32, prop)
     e.set_option(L.SDK_OPT_ORDER, order)
+    for k, v in opts:
+        e.set_option(k, v)
     e.solve_batch(boards[:8192])
     e.timer_reset()
     t = time.perf_counter()
@@ -72,7 +74,18 @@ def run(e, boards, prop, order):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--variants", default="default",
+                    help="comma list of prop32 settings to check: default, nohandover, tail<live>x<step>")
     args = ap.parse_args()
+    variants = []
+    for v in args.variants.split(","):
+        if v == "default":
+            variants.append((v, ((L.SDK_OPT_PROP32_HANDOVER, 1), (L.SDK_OPT_PROP32_TAIL, 0))))
+        elif v == "nohandover":
+            variants.append((v, ((L.SDK_OPT_PROP32_HANDOVER, 0), (L.SDK_OPT_PROP32_TAIL, 0))))
+        elif v.startswith("tail"):
+            live, step = (int(t) for t in v[4:].split("x"))
+            variants.append((v, ((L.SDK_OPT_PROP32_HANDOVER, 1), (L.SDK_OPT_PROP32_TAIL, live | step << 8))))
     e = SudokuEngine(0)
     q = args.quick
     work = [
@@ -86,15 +99,16 @@ def main():
     bad = 0
     for name, boards in work:
         for order, oname in ((L.SDK_ORDER_LEX, "lex"), (L.SDK_ORDER_MRV_UNIQUE, "mrv")):
-            o0, s0, ms0, w0, _ = run(e, boards, 0, order)
-            o1, s1, ms1, w1, und = run(e, boards, 1, order)
+          o0, s0, ms0, w0, _ = run(e, boards, 0, order)
+          for vname, opts in variants:
+            o1, s1, ms1, w1, und = run(e, boards, 1, order, opts)
             mo = int(np.count_nonzero((o0 != o1).any(axis=1)))
             ms_ = int(np.count_nonzero(s0 != s1))
             bad += mo + ms_
             stc = {int(k): int(v) for k, v in zip(*np.unique(s1, return_counts=True))}
-            print(f"{name:12s} {oname} n={len(boards):8d} undecided={und:8d} out_mismatch={mo} status_mismatch={ms_} "
-                  f"solve_ms off={ms0:8.3f} on={ms1:8.3f} speedup={ms0 / max(ms1, 1e-9):5.2f} statuses={stc}",
-                  flush=True)
+            print(f"{name:12s} {oname} {vname:10s} n={len(boards):8d} undecided={und:8d} out_mismatch={mo} "
+                  f"status_mismatch={ms_} solve_ms off={ms0:8.3f} on={ms1:8.3f} speedup={ms0 / max(ms1, 1e-9):5.2f} "
+                  f"statuses={stc}", flush=True)
             if mo or ms_:
                 i = int(np.flatnonzero((o0 != o1).any(axis=1) | (s0 != s1))[0])
                 print("  first mismatch", i, "status", s0[i], s1[i])

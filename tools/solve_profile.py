@@ -32,6 +32,7 @@ ap.add_argument("--helpers", type=int, default=0, help="QUAD: SDK_OPT_DONATE_HEL
 ap.add_argument("--resume", type=int, default=-1, help="QUAD: SDK_OPT_DONATE_RESUME (default: library default)")
 ap.add_argument("--prop32", type=int, default=-1, help="QUAD: SDK_OPT_PROP32 (default: library default)")
 ap.add_argument("--prop32-lc", type=int, default=0, help="QUAD: SDK_OPT_PROP32_LC (0: library default)")
+ap.add_argument("--prop32-tail", type=int, default=-1, help="QUAD: SDK_OPT_PROP32_TAIL (live | step << 8)")
 args = ap.parse_args()
 
 if args.workload == "minimal":
@@ -71,6 +72,8 @@ with SudokuEngine(0) as eng:
         eng.set_option(L.SDK_OPT_PROP32, args.prop32)
     if args.prop32_lc and hasattr(L, "SDK_OPT_PROP32_LC"):
         eng.set_option(L.SDK_OPT_PROP32_LC, args.prop32_lc)
+    if args.prop32_tail >= 0:
+        eng.set_option(L.SDK_OPT_PROP32_TAIL, args.prop32_tail)
     d_in, d_out, d_st = eng.alloc(args.n * 81), eng.alloc(args.n * 81), eng.alloc(args.n)
     d_in.upload(p)
     eng.solve_batch_dev(d_in, d_out, d_st, args.n)
@@ -83,7 +86,8 @@ with SudokuEngine(0) as eng:
     out = np.empty((args.n, 81), np.uint8)
     d_out.download(out)
     per = ms / args.reps       # one solve: one launch, or both launches of a two-phase solve
-    p32 = f" p32={args.prop32}/{args.prop32_lc}" if args.prop32 >= 0 or args.prop32_lc else ""
+    p32 = (f" p32={args.prop32}/{args.prop32_lc}/t{args.prop32_tail}"
+           if args.prop32 >= 0 or args.prop32_lc or args.prop32_tail >= 0 else "")
     print(f"{args.solver} {args.order} lc={args.locked} xh={args.xcd_heads} dn={args.donate}/{args.donate_mode}/h{args.helpers} chunk={args.chunk}{p32} {args.workload} n={args.n} solve={per:.3f} ms "
           f"({nl // args.reps} launches) rate={args.n / per * 1e3 / 1e6:.1f} M/s ok={(out == s).all()}", flush=True)
     if args.sweep:

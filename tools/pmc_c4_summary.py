@@ -105,6 +105,11 @@ def main(d):
             ("c4", C4_PUZZLES, "sdk::solve", cal.get("read_correction"), cal.get("write_correction"),
              "FETCH/WRITE_SIZE scaled by tools/fetch_calib's algorithmic/counter ratios for the solvers' "
              "byte-load/byte-store pattern", (81, 82)),
+            # round 5: the C4 boards are decided by the propagation pass, which moves whole groups
+            # (5184 B) with 16-B loads and stores, the checker's access pattern
+            ("c4", C4_PUZZLES, "sdk::prop32", 2.0, 1.0,
+             "2 x FETCH_SIZE (gfx950: FETCH_SIZE reports half of a 16-B/lane read, as for the checker) + "
+             "WRITE_SIZE (16-B stores)", (81, 82)),
             ("c3", C3_BOARDS, "sdk::check_kernel", 2.0, 1.0,
              "2 x FETCH_SIZE (gfx950: FETCH_SIZE reports half of a 16-B/lane streaming read) + WRITE_SIZE", (81, 1)),
             ("min", MIN_PUZZLES, "sdk::solve4_kernel", None, None, None, None),

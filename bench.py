@@ -525,7 +525,7 @@ def hard_leg(eng, d, args, synth, L):
             checked += d.world * len(bp)
             legs[mode] = {"value": d.world * len(bp) / el, "unit": "puzzles/s", "ms": el * 1000.0,
                           "order": "lex" if order == L.SDK_ORDER_LEX else "mrv_unique",
-                          "split_budget": dn if dn > 1 else (128 if dn else None),
+                          "split_budget": dn if dn > 1 else ((256 if len(bp) > (1 << 19) else 128) if dn else None),
                           "split_boards": eng.get_option(L.SDK_OPT_SPLIT_BOARDS),
                           "lex_boards": eng.get_option(L.SDK_OPT_LEX_BOARDS),
                           "donated": eng.get_option(L.SDK_OPT_DONATED)}

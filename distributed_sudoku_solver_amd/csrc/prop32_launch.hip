@@ -13,7 +13,7 @@ hipError_t launch_prop32(const Prop32Args& a, unsigned grid, hipStream_t stream)
 
 hipError_t launch_p32_scatter(const uint32_t* list, const uint8_t* sub_out, const int8_t* sub_st, const uint8_t* in,
                               uint8_t* out, int8_t* status, unsigned grid, hipStream_t stream) {
-    p32_scatter_kernel<<<grid, 128, 0, stream>>>(list, sub_out, sub_st, in, out, status);
+    p32_scatter_kernel<<<grid, 256, 0, stream>>>(list, sub_out, sub_st, in, out, status);
     return hipGetLastError();
 }
 

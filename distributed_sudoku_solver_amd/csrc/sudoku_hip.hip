@@ -742,11 +742,18 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
         ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15u) == 0)
         return launch_prop32_solve(c, d_in, d_out, d_status, n, order, budget, donate);
     const int64_t dn = donate >= 0 ? donate : (int64_t)c->donate;
-    const uint64_t split = dn == 1 ? kDnSplitDefault : (uint64_t)dn;
+    // the default split budget doubles above 2^19 boards: with ~30 boards per slot a heavy board's
+    // extra nodes overlap the bulk, and fewer boards reach the donation launch (1M hard boards, LEX:
+    // 6.88 ms at 128, 6.14 at 256, 6.39 at 384; 100k: 1.90 / 2.04 at 128 / 256;
+    // profiles/r05/sweep_phased_hard_r05s.log)
+    const uint64_t split = dn == 1 ? (n > (1u << 19) ? 2 * kDnSplitDefault : kDnSplitDefault) : (uint64_t)dn;
     const bool two_phase = n > 0 && !count_mode && dn && c->solver == SDK_SOLVER_QUAD &&
                            (eff_order == SDK_ORDER_LEX || eff_order == SDK_ORDER_MRV_UNIQUE) && d_out && d_status &&
                            (node_budget == 0 || node_budget > split) &&
-                           (c->dn_max == 0 || (int64_t)n <= c->dn_max);
+                           // a prop32 fallback batch (n_dev) holds only boards propagation left open:
+                           // phased at any size (1M hard boards: 6.8 ms phased vs 8.3 in one launch,
+                           // profiles/r05/ab_dnmax_r05r.log)
+                           (c->dn_max == 0 || (int64_t)n <= c->dn_max || n_dev);
     c->dn_ran = two_phase;
     if (two_phase) c->dn_err_check = true;
     // resumed items keep the split phase's branching, so only MRV stacks resume, into the
@@ -829,7 +836,8 @@ int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t*
                       static_cast<int8_t*>(c->p32_st.p), nullptr, n, 0, 0, nullptr, nullptr, 0, 1, order, budget,
                       donate, lst);
     if (!rc) {
-        const unsigned g = (unsigned)std::min<uint64_t>(n, (uint64_t)c->cus * 16);
+        // one thread per byte of the list's boards (its length is on the device: sized for all n)
+        const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n * 81 + 255) / 256, (uint64_t)c->cus * 8));
         if (sdk::launch_p32_scatter(lst, static_cast<uint8_t*>(c->p32_out.p), static_cast<int8_t*>(c->p32_st.p), d_in,
                                     d_out, d_status, g, c->stream) != hipSuccess)
             rc = fail(SDK_EHIP, "prop32 scatter launch failed");

@@ -1883,6 +1883,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         n = min<uint64_t>(*args.n_dev, args.n);
         if (n == 0) return;
     }
+    const uint64_t budget = (args.budget_big && n > kBudgetBigBoards) ? args.budget_big : args.budget;
     __shared__ uint2 s_region[2 * kRegion4];
     __shared__ uint8_t s_in[2 * 2 * 81];
     __shared__ uint2 s_stk[kLds4Levels > 0 ? kLds4Levels : 1][2][64];   // unused when kLds4Levels = 0
@@ -1911,7 +1912,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
     a.status = args.status;
     a.work = args.work;
     a.work_rounds = args.work_rounds;
-    a.budget = args.budget;
+    a.budget = budget;
     a.iter = 0;
     a.locked = args.locked;
     a.heads = args.heads;

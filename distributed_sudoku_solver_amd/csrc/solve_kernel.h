@@ -84,10 +84,14 @@ struct SolveArgs {
     void* save = nullptr;      // QUAD split phase: stacks of boards that reach the split budget
                                // (solve4_kernel.h SplitSave; nullable)
     uint32_t* save_idx = nullptr;   // ... and each saved board's entry (by board index)
+    uint64_t budget_big = 0;        // QUAD split phase of a device-counted batch (n_dev): the budget
+                                    // when more than kBudgetBigBoards boards are searched (0 = budget)
     long long* found = nullptr;     // QUAD first-solution scan (sdk_frontier_first): the lowest board
                                     // index (in_first + i * in_step) with status 1 or -2 so far; boards
                                     // above it are cancelled (solve4_kernel.h, s_found4)
 };
+// the phased solve's default split budget doubles above this many searched boards (sudoku_hip.hip)
+constexpr uint64_t kBudgetBigBoards = 1ull << 19;
 // status of a board a first-solution scan stopped because it lies above a lower board's hit
 constexpr int kStCancelled = -3;
 

@@ -319,6 +319,8 @@ struct sdk_ctx {
     int64_t dn_max = 1 << 19;      // largest batch solved in phases (SDK_OPT_DONATE_MAX, 0 = any)
     uint32_t dn_epoch = 0;         // launches that used it (mailbox / registration entries carry it)
     int dn_blocks_per_cu = 0;      // resident solve4_kernel<true> workgroups per CU (queried once)
+    uint64_t split_big = 0;        // the phased solve being enqueued: its split budget above
+                                   // sdk::kBudgetBigBoards searched boards (device-counted batches)
     int prop32 = 1;                // QUAD: bit-sliced root propagation first (SDK_OPT_PROP32)
     int prop32_lc = 4;             // ... a locked-candidates pass every this many steps
     int64_t prop32_min = 4096;     // ... for batches of at least this many boards
@@ -545,6 +547,7 @@ int launch_solve_once(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, u
     a.save_idx = nullptr;
     // a first-solution scan (frontier_first): the plain QUAD launch cancels boards above the lowest hit
     a.found = (four && !count_mode && dn_phase == 0) ? c->first_found : nullptr;
+    a.budget_big = (four && dn_phase == 1) ? c->split_big : 0;   // the split phase of a device-counted batch
     if (dn_phase == 1 && c->dn_resume_now && four && !count_mode) {
         // the split phase leaves the stacks of the boards it stops (sdk::split_save4)
         a.save = c->dn_save.p;
@@ -742,11 +745,16 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
         ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15u) == 0)
         return launch_prop32_solve(c, d_in, d_out, d_status, n, order, budget, donate);
     const int64_t dn = donate >= 0 ? donate : (int64_t)c->donate;
-    // the default split budget doubles above 2^19 boards: with ~30 boards per slot a heavy board's
-    // extra nodes overlap the bulk, and fewer boards reach the donation launch (1M hard boards, LEX:
-    // 6.88 ms at 128, 6.14 at 256, 6.39 at 384; 100k: 1.90 / 2.04 at 128 / 256;
-    // profiles/r05/sweep_phased_hard_r05s.log)
-    const uint64_t split = dn == 1 ? (n > (1u << 19) ? 2 * kDnSplitDefault : kDnSplitDefault) : (uint64_t)dn;
+    // the default split budget doubles above 2^19 SEARCHED boards (sdk::kBudgetBigBoards; a prop32
+    // fallback batch's count is on the device, so its split launch picks the budget there): with ~30
+    // boards per slot a heavy board's extra nodes overlap the bulk, and fewer boards reach the
+    // donation launch (1M hard boards, 880k searched, LEX: 6.88 ms at 128, 6.14 at 256, 6.39 at 384;
+    // 1M minimal, 460k searched: 2.68 ms at 128, 2.93 at 256; profiles/r05/sweep_phased_hard_r05s.log,
+    // ab_lc_r05t.log)
+    const bool split_auto = dn == 1;
+    const uint64_t split = split_auto ? (!n_dev && n > sdk::kBudgetBigBoards ? 2 * kDnSplitDefault : kDnSplitDefault)
+                                      : (uint64_t)dn;
+    c->split_big = split_auto && n_dev ? 2 * kDnSplitDefault : 0;
     const bool two_phase = n > 0 && !count_mode && dn && c->solver == SDK_SOLVER_QUAD &&
                            (eff_order == SDK_ORDER_LEX || eff_order == SDK_ORDER_MRV_UNIQUE) && d_out && d_status &&
                            (node_budget == 0 || node_budget > split) &&

@@ -55,6 +55,8 @@ constexpr uint32_t kP32URec = 72;        // bytes per unit record: (T_d, once_d)
 constexpr uint32_t kP32TRec = 40;        // bytes per triad record: 9 words + pad
 constexpr uint32_t kP32ColTri = 1280;    // the column triads' records (32 row-triad slots before)
 constexpr uint32_t kP32Region = 3456;    // bytes per half: 86 cell records (81 + the spare lanes')
+constexpr uint32_t kP32Table = 2 * kP32Region;   // p32_unit's read order, 48 B per lane (p32_order_table)
+constexpr uint32_t kP32Lds = kP32Table + 32 * 48;
 constexpr uint32_t kP32Stage = 2592;     // bytes per half of the group's boards (32 x 81)
 constexpr uint32_t kP32Heads = 8;        // dequeue counters, one per XCD segment of the groups
 constexpr uint32_t kP32HeadStride = 32;  // words between counters (own cache lines)
@@ -128,14 +130,24 @@ __device__ __forceinline__ void p32_singles(const P32Lane& w, P32Cells& x, uint3
     alls = ~0u;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        uint32_t a1 = x.c[k][0], a2 = 0u;
-#pragma unroll
-        for (int d = 1; d < 9; ++d) {
-            a2 |= a1 & x.c[k][d];
-            a1 |= x.c[k][d];
-        }
-        x.s[k] = a1 & ~a2;
-        empty |= ~a1;
+        // exactly one of nine words: "in two or more" by majorities, three words then pairs (10
+        // instructions instead of the 17 of a one-word-at-a-time chain)
+        const uint32_t* c = x.c[k];
+        uint32_t o, w2, t1, t2, t3;
+        asm("v_or3_b32 %[o], %[c0], %[c1], %[c2]\n\t"
+            "v_bitop3_b32 %[w], %[c0], %[c1], %[c2] bitop3:0xe8\n\t"
+            "v_bitop3_b32 %[t1], %[o], %[c3], %[c4] bitop3:0xe8\n\t"
+            "v_or3_b32 %[o], %[o], %[c3], %[c4]\n\t"
+            "v_bitop3_b32 %[t2], %[o], %[c5], %[c6] bitop3:0xe8\n\t"
+            "v_or3_b32 %[o], %[o], %[c5], %[c6]\n\t"
+            "v_bitop3_b32 %[t3], %[o], %[c7], %[c8] bitop3:0xe8\n\t"
+            "v_or3_b32 %[o], %[o], %[c7], %[c8]\n\t"
+            "v_or3_b32 %[w], %[w], %[t1], %[t2]"
+            : [o] "=&v"(o), [w] "=&v"(w2), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+            : [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]),
+              [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]));
+        x.s[k] = o & ~(w2 | t3);
+        empty |= ~o;
         alls &= x.s[k];
     }
     if (!w.act) return;   // spare lanes store nothing: their reads below return whatever is there
@@ -262,10 +274,20 @@ __device__ __forceinline__ uint32_t p32_dups(const P32Lane& w) {
     return dup;
 }
 
-__device__ __forceinline__ void p32_unit(const P32Lane& w, uint32_t& miss) {
-    const uint32_t j = p32_opq(w.hl);
-    uint32_t u0, ua, ub;
-    p32_unit_cells(j, u0, ua, ub);
+// The unit phase's read order.  Step t of every unit lane reads the cell of its unit where the fixed
+// grid kP32Order holds t: kP32Order is a valid Sudoku solution, so at each step the 27 lanes read the
+// same nine cells (one per row, column and box -- each by three lanes, a broadcast), and it is chosen
+// so that those nine cells' records (40 B apart) fall in nine different bank pairs (cell index mod 32
+// distinct in every digit class; found by a search over relabelled and permuted pattern grids).  The
+// natural order met two addresses per bank pair on every read (15-16 % of the launch's LDS cycles
+// were bank conflicts).  The per-lane offsets are a table in LDS (12 words per lane, 3 reads a step).
+__device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds, uint32_t& miss) {
+    const uint32_t j = p32_opq(w.hl);   // the unit record written below
+    const __attribute__((address_space(3))) p32_u4* tb =
+        (const __attribute__((address_space(3))) p32_u4*)(lds + kP32Table + 48u * w.hl);
+    const p32_u4 ta = tb[0], tc = tb[1];
+    const uint32_t t8 = *(const __attribute__((address_space(3))) uint32_t*)(lds + kP32Table + 48u * w.hl + 32u);
+    const uint32_t ord[9] = {ta[0], ta[1], ta[2], ta[3], tc[0], tc[1], tc[2], tc[3], t8};
     uint32_t ones[9], twos[9], T[9];
 #if SDK_PROP32_UNIT_PAIR
     // cells 0, 1 (ten fewer registers than three at a time), then pairs (2, 3) .. (6, 7), then cell 8
@@ -323,7 +345,7 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, uint32_t& miss) {
         uint32_t a[3][9], s[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            const uint32_t o = u0 + (uint32_t)q * ua;
+            const uint32_t o = ord[q];
             const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
                         r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
             a[q][0] = r0.x; a[q][1] = r0.y; a[q][2] = r1.x; a[q][3] = r1.y; a[q][4] = r2.x;
@@ -349,7 +371,7 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, uint32_t& miss) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int q = 3 + 2 * p + h;
-            const uint32_t o = u0 + (uint32_t)(q % 3) * ua + (uint32_t)(q / 3) * ub;
+            const uint32_t o = ord[q];
             const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
                         r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
             a[h][0] = r0.x; a[h][1] = r0.y; a[h][2] = r1.x; a[h][3] = r1.y; a[h][4] = r2.x;
@@ -628,13 +650,37 @@ __global__ void p32_scatter_kernel(const uint32_t* list, const uint8_t* sub_out,
     }
 }
 
+// kP32Order (see p32_unit): digit class t of a Sudoku solution with cell indices distinct mod 32
+// in every class
+__constant__ uint8_t kP32Order[81] = {2, 5, 8, 1, 4, 7, 3, 0, 6, 1, 4, 7, 0, 3, 6, 2, 8, 5, 0, 3, 6, 8, 2, 5, 1,
+                                      7, 4, 8, 2, 5, 7, 1, 4, 0, 6, 3, 7, 1, 4, 6, 0, 3, 8, 5, 2, 6, 0, 3, 5, 8,
+                                      2, 7, 4, 1, 5, 8, 2, 4, 7, 1, 6, 3, 0, 4, 7, 1, 3, 6, 0, 5, 2, 8, 3, 6, 0,
+                                      2, 5, 8, 4, 1, 7};
+
+// p32_unit's per-lane read order, lane j at kP32Table + 48 j: word t = the record offset of the cell
+// of unit j whose kP32Order entry is t.  Spare lanes take lane 0's (one more reader of each address).
+// Written once per workgroup.
+__device__ __forceinline__ void p32_order_table(p32_lds_t* lds) {
+    if (threadIdx.x >= 32) return;
+    uint32_t u0, ua, ub;
+    p32_unit_cells(threadIdx.x < 27 ? threadIdx.x : 0u, u0, ua, ub);
+    __attribute__((address_space(3))) uint32_t* tab =
+        (__attribute__((address_space(3))) uint32_t*)(lds + kP32Table + 48u * threadIdx.x);
+    for (uint32_t q = 0; q < 9; ++q) {
+        const uint32_t o = u0 + (q % 3) * ua + (q / 3) * ub;
+        tab[kP32Order[o / kP32Rec]] = o;
+    }
+}
+
 #ifndef SDK_PROP32_WAVES_PER_EU
 #define SDK_PROP32_WAVES_PER_EU 4
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_WAVES_PER_EU))) void prop32_kernel(
     Prop32Args a) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[2 * kP32Region];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[kP32Lds];
     p32_lds_t* const lds = (p32_lds_t*)s_lds;
+    p32_order_table(lds);
+    __builtin_amdgcn_wave_barrier();
     P32Lane w;
     w.half = threadIdx.x >> 5;
     w.hl = threadIdx.x & 31;
@@ -729,7 +775,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
                 live &= ~dupw;
             }
             uint32_t miss;
-            p32_unit(w, miss);
+            p32_unit(w, lds, miss);
             const uint64_t badw = p32_mask64(p32_half_or(w.act ? (miss | empty) : 0u));
             const uint64_t allw = p32_mask64(p32_half_and(w.act ? alls : ~0u));
             const uint64_t sv = allw & ~badw & live, ct = badw & live;

@@ -90,6 +90,12 @@ def parse_args():
                     help="hard-search leg: the committed hard set (100k distinct puzzles that search) and its "
                          "1000 heaviest, one launch vs the phased solve with subtree donation (0 = skip)")
     ap.add_argument("--hard-reps", type=int, default=10, help="hard_1m: symmetries of the 100k hard set per GPU")
+    ap.add_argument("--prop32", type=int, default=-1, help="SDK_OPT_PROP32 for every leg (-1 = library default)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="NAME=VALUE: an SDK_OPT_* engine option for every leg (experiments), e.g. PROP32_LC=3")
+    ap.add_argument("--hard-inflight", type=int, default=3,
+                    help="hard legs: passes in flight of the donation_in_flight mode (0 = --inflight); 3: the "
+                         "hard sets' launch tails are longer than C4's (profiles/r05/bench_hard_inflight_r05z.log)")
     ap.add_argument("--count-leg", type=int, default=1, help="C5 leg: frontier-split count over all ranks (0 = skip)")
     ap.add_argument("--c5-boards", default="15,14",
                     help="C5 boards: 16/15/14 clues (S1 with clues removed; counts 7,309 / 3,481,026 / 18,204,270); "
@@ -458,28 +464,44 @@ def minimal_leg(eng, d, args, synth, L):
             "search": stats, "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
 
 
-def _timed_solves(eng, d, p, s, steps):
-    """Wall time of `steps` solve_batch_dev passes over resident boards (+ 1 warm-up), max over
-    ranks; every board checked against its known answer afterwards."""
+def _timed_solves(eng, d, p, s, steps, contexts=1):
+    """Wall time of `steps` solve_batch_dev passes over resident boards (+ 1 warm-up per context),
+    max over ranks; every board of every output buffer checked against its known answer afterwards.
+    contexts > 1: consecutive passes on that many engine contexts in turn (own stream and output
+    buffers each, engine.fork()), as the headline's passes in flight -- one pass's launch tail (a few
+    heavy boards on a nearly idle GPU) overlaps the next pass."""
     n = len(p)
-    d_in, d_out, d_st = eng.alloc(n * 81), eng.alloc(n * 81), eng.alloc(n)
+    engines = [eng] + [eng.fork() for _ in range(max(1, contexts) - 1)]
+    d_in = eng.alloc(n * 81)
+    bufs = [(e.alloc(n * 81), e.alloc(n)) for e in engines]
     d_in.upload(p)
-    eng.solve_batch_dev(d_in, d_out, d_st, n)
-    eng.synchronize()
+    for e, (d_out, d_st) in zip(engines, bufs):
+        e.solve_batch_dev(d_in, d_out, d_st, n)
+    for e in engines:
+        e.synchronize()
     d.barrier()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        eng.solve_batch_dev(d_in, d_out, d_st, n)
-    eng.synchronize()
+    for i in range(steps):
+        k = i % len(engines)
+        engines[k].solve_batch_dev(d_in, bufs[k][0], bufs[k][1], n)
+    for e in engines:
+        e.synchronize()
     d.barrier()
     el = d.max(time.perf_counter() - t0) / steps
     out = np.empty((n, 81), np.uint8)
     st = np.empty(n, np.int8)
-    d_out.download(out)
-    d_st.download(st)
-    bad = int(d.sum(int(((out != s).any(axis=1) | (st != 1)).sum())))
-    for b in (d_in, d_out, d_st):
-        b.free()
+    bad = 0
+    for d_out, d_st in bufs:
+        d_out.download(out)
+        d_st.download(st)
+        bad += int(((out != s).any(axis=1) | (st != 1)).sum())
+    bad = int(d.sum(bad))
+    d_in.free()
+    for d_out, d_st in bufs:
+        d_out.free()
+        d_st.free()
+    for e in engines[1:]:
+        e.close()
     return el, bad
 
 
@@ -514,16 +536,21 @@ def hard_leg(eng, d, args, synth, L):
     split_dn = {"heaviest_1000": 16}
     for name, (bp, bs) in (("hard_100k", (p, s)), ("heaviest_1000", (hp, hs)), ("hard_1m", (mp, ms))):
         legs = {}
-        for mode, order, dn in (("one_launch", L.SDK_ORDER_LEX, 0), ("donation", L.SDK_ORDER_LEX, split_dn.get(name, 1)),
-                                ("mrv_one_launch", L.SDK_ORDER_MRV_UNIQUE, 0),
-                                ("mrv_donation", L.SDK_ORDER_MRV_UNIQUE, split_dn.get(name, 1))):
+        for mode, order, dn, ctx in (("one_launch", L.SDK_ORDER_LEX, 0, 1),
+                                     ("donation", L.SDK_ORDER_LEX, split_dn.get(name, 1), 1),
+                                     ("mrv_one_launch", L.SDK_ORDER_MRV_UNIQUE, 0, 1),
+                                     ("mrv_donation", L.SDK_ORDER_MRV_UNIQUE, split_dn.get(name, 1), 1),
+                                     ("donation_in_flight", L.SDK_ORDER_LEX, split_dn.get(name, 1),
+                                      args.hard_inflight or args.inflight)):
+            if ctx < 2 and mode == "donation_in_flight":
+                continue
             eng.set_option(L.SDK_OPT_ORDER, order)
             eng.set_option(L.SDK_OPT_DONATE, dn)
             eng.set_option(L.SDK_OPT_DONATE_MAX, 0)       # phased at any size (hard_1m is above the default)
-            el, b = _timed_solves(eng, d, bp, bs, 5)
+            el, b = _timed_solves(eng, d, bp, bs, 6 if ctx > 1 else 5, contexts=ctx)
             bad += b
-            checked += d.world * len(bp)
-            legs[mode] = {"value": d.world * len(bp) / el, "unit": "puzzles/s", "ms": el * 1000.0,
+            checked += d.world * len(bp) * ctx
+            legs[mode] = {"value": d.world * len(bp) / el, "unit": "puzzles/s", "ms": el * 1000.0, "contexts": ctx,
                           "order": "lex" if order == L.SDK_ORDER_LEX else "mrv_unique",
                           "split_budget": dn if dn > 1 else ((256 if len(bp) > (1 << 19) else 128) if dn else None),
                           "split_boards": eng.get_option(L.SDK_OPT_SPLIT_BOARDS),
@@ -534,7 +561,8 @@ def hard_leg(eng, d, args, synth, L):
         eng.set_option(L.SDK_OPT_DONATE_MAX, old_max)
         base = legs["one_launch"]["value"]
         legs["donation_speedup"] = legs["donation"]["value"] / base
-        best = max(("donation", "mrv_one_launch", "mrv_donation"), key=lambda m: legs[m]["value"])
+        best = max((m for m in ("donation", "mrv_one_launch", "mrv_donation", "donation_in_flight") if m in legs),
+                   key=lambda m: legs[m]["value"])
         legs["best"] = {"mode": best, "speedup_vs_lex_one_launch": legs[best]["value"] / base}
         res[name] = legs
     res["hard_1m"]["workload"] = f"the {len(p)} hard puzzles x {reps} seeded symmetries ({len(mp)} boards) per GPU"
@@ -551,7 +579,7 @@ def hard_leg(eng, d, args, synth, L):
     res["workload"] = (f"{len(p)} distinct hard puzzles per GPU ({int((p > 0).sum(1).mean())} clues on average, "
                        f"committed set) and their 1000 heaviest, resident in HBM")
     res["search"] = stats
-    res["parity"] = {"mismatched_boards": bad, "checked_boards": 5 * checked}   # every mode, every board
+    res["parity"] = {"mismatched_boards": bad, "checked_boards": checked}   # every mode, every output buffer
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
         res["cpu_baseline_c_port"] = cpu_baseline_c(p, min(args.cpu_seconds, 5.0), cpu_share())
     return res
@@ -578,6 +606,11 @@ def lane_dfs_leg(eng, args, synth, L):
     finally:
         eng.set_option(L.SDK_OPT_NODE_BUDGET, 0)
         eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
+    if args.prop32 >= 0:
+        eng.set_option(L.SDK_OPT_PROP32, args.prop32)
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        eng.set_option(getattr(L, "SDK_OPT_" + k), int(v))
     # the same batch with the per-puzzle budget cut to 20k validations: the wave-parallel bulk
     # rate without the serial tail of the few boards that need a million validations
     eng.set_option(L.SDK_OPT_SOLVER, L.SDK_SOLVER_LANE)
@@ -589,6 +622,11 @@ def lane_dfs_leg(eng, args, synth, L):
     finally:
         eng.set_option(L.SDK_OPT_NODE_BUDGET, 0)
         eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
+    if args.prop32 >= 0:
+        eng.set_option(L.SDK_OPT_PROP32, args.prop32)
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        eng.set_option(getattr(L, "SDK_OPT_" + k), int(v))
     m = min(n, 4096)
     cores = args.cpu_cores or cpu_share()
     t1 = time.perf_counter()
@@ -793,6 +831,11 @@ def main():
         args.shared_gpus = d.world > ndev.value
     eng.set_option(L.SDK_OPT_ORDER, L.SDK_ORDER_LEX if args.order == "lex" else L.SDK_ORDER_MRV_UNIQUE)
     eng.set_option(L.SDK_OPT_SOLVER, SOLVERS[args.solver][0])
+    if args.prop32 >= 0:
+        eng.set_option(L.SDK_OPT_PROP32, args.prop32)
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        eng.set_option(getattr(L, "SDK_OPT_" + k), int(v))
     if args.waves_per_cu:
         eng.set_option(SOLVERS[args.solver][2], args.waves_per_cu)
     solve_kernel = SOLVERS[args.solver][1]

@@ -131,8 +131,12 @@ def solo(b):
 
 def lockstep(group, policy, lc_every):
     """All boards of the group take every step.  policy 'fix': an LC pass after a singles round in
-    which some live board made no change; 'every': an LC pass after every lc_every-th round."""
+    which some live board made no change; 'every': an LC pass after every lc_every-th round;
+    'stall': after a round in which no live board closed a cell, or after lc_every rounds without a
+    pass."""
     Xs = [board_state(b) for b in group]
+    prev_closed = [sum(single(x) for x in X) for X in Xs]
+    since = 0
     live = [True] * len(group)
     kinds = [None] * len(group)
     rounds = lcs = 0
@@ -150,8 +154,16 @@ def lockstep(group, policy, lc_every):
                 fix = True
                 kinds[i] = "fix"
         rounds += 1
-        run_lc = fix if policy == "fix" else (rounds % lc_every == 0 or (fix and all(
-            kinds[i] == "fix" for i in range(len(group)) if live[i])))
+        since = locals().get("since", 0) + 1
+        if policy == "stall":
+            closed_any = any(sum(single(x) for x in Xs[i]) > prev_closed[i] for i in range(len(group)) if live[i])
+            run_lc = (not closed_any) or since >= lc_every
+        else:
+            run_lc = fix if policy == "fix" else (rounds % lc_every == 0 or (fix and all(
+                kinds[i] == "fix" for i in range(len(group)) if live[i])))
+        prev_closed = [sum(single(x) for x in X) for X in Xs]
+        if run_lc:
+            since = 0
         if run_lc and any(live):
             lcs += 1
             for i, X in enumerate(Xs):
@@ -184,7 +196,7 @@ def main():
     kinds = [x[2] for x in res]
     print(f"solo: rounds mean {r.mean():.2f} max {r.max()}, LC passes mean {lc.mean():.2f}, "
           f"solved {kinds.count('solved')}, stuck {kinds.count('stuck')}, contra {kinds.count('contra')}")
-    for policy, k in (("fix", 0), ("every", 2), ("every", 3), ("every", 4)):
+    for policy, k in (("every", 1), ("every", 2), ("every", 3)):
         gr, gl, stuck = [], [], 0
         for g in range(0, len(p), args.group):
             rr, ll, kk = lockstep(p[g:g + args.group], policy, k)

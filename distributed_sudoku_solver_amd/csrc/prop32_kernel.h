@@ -23,10 +23,11 @@
 //   singles:  s = exactly-one over the nine words, empty = no candidate, and the cell records
 //             (9 candidate words + s) written to LDS;
 //   unit:     the lane's unit over its nine cell records -- T (digits of its closed cells),
-//             once (digits in exactly one cell), missing digits (contradiction) -- written as
-//             (T_d, once_d) pairs;
+//             twos (digits in two or more cells), missing digits (contradiction) -- written as
+//             (T_d, twos_d) pairs;
 //   cells:    each cell loses the T of its three units unless closed, takes a hidden single
-//             (a remaining candidate in some unit's once), and "changed" is accumulated.
+//             (a remaining candidate not in some unit's twos: the cell itself holds it, so that
+//             unit holds it once), and "changed" is accumulated.
 // After every lc_every-th step the next step's unit/cell phases are replaced by one
 // locked-candidates pass over the 54 box-line triads:
 //   presence P(triad) = OR of its three cells' words (closed cells included, so the pass is sound at
@@ -51,12 +52,12 @@ namespace sdk {
 constexpr int kStUndecided = -4;
 
 constexpr uint32_t kP32Rec = 40;         // bytes per cell record: 9 candidate words, the single word
-constexpr uint32_t kP32URec = 72;        // bytes per unit record: (T_d, once_d), d = 0..8
+constexpr uint32_t kP32URec = 72;        // bytes per unit record: (T_d, twos_d), d = 0..8
 constexpr uint32_t kP32TRec = 40;        // bytes per triad record: 9 words + pad
 constexpr uint32_t kP32ColTri = 1280;    // the column triads' records (32 row-triad slots before)
 constexpr uint32_t kP32Region = 3456;    // bytes per half: 86 cell records (81 + the spare lanes')
-constexpr uint32_t kP32Table = 2 * kP32Region;   // p32_unit's read order, 48 B per lane (p32_order_table)
-constexpr uint32_t kP32Lds = kP32Table + 32 * 48;
+constexpr uint32_t kP32Table = 2 * kP32Region;   // p32_unit's read order, 40 B per lane (p32_order_table)
+constexpr uint32_t kP32Lds = kP32Table + 64 * 40;
 constexpr uint32_t kP32Stage = 2592;     // bytes per half of the group's boards (32 x 81)
 constexpr uint32_t kP32Heads = 8;        // dequeue counters, one per XCD segment of the groups
 constexpr uint32_t kP32HeadStride = 32;  // words between counters (own cache lines)
@@ -98,6 +99,10 @@ typedef __attribute__((address_space(3))) uint8_t p32_lds_t;
 typedef unsigned int p32_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint2 p32_ld(p32_lds_t* base, uint32_t off) {
     const uint64_t v = *(const volatile __attribute__((address_space(3))) uint64_t*)(base + off);
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+__device__ __forceinline__ uint2 p32_lda(uint32_t addr) {   // an absolute LDS address
+    const uint64_t v = *(const volatile __attribute__((address_space(3))) uint64_t*)(uintptr_t)addr;
     return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 }
 __device__ __forceinline__ void p32_st(p32_lds_t* base, uint32_t off, uint32_t x, uint32_t y) {
@@ -150,11 +155,12 @@ __device__ __forceinline__ void p32_singles(const P32Lane& w, P32Cells& x, uint3
         empty |= ~o;
         alls &= x.s[k];
     }
-    if (!w.act) return;   // spare lanes store nothing: their reads below return whatever is there
+    // spare lanes store into record 81 (no branch: a divergent region inside the step loop cost the
+    // cell words a second register home); their unit reads return whatever is there
     const uint32_t rec = kP32Rec * p32_opq(w.hl);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const uint32_t o = rec + 1080u * k;
+        const uint32_t o = w.act ? rec + 1080u * k : 81u * kP32Rec;
         p32_st(w.reg, o, x.c[k][0], x.c[k][1]);
         p32_st(w.reg, o + 8, x.c[k][2], x.c[k][3]);
         p32_st(w.reg, o + 16, x.c[k][4], x.c[k][5]);
@@ -189,7 +195,8 @@ __device__ __forceinline__ void p32_unit2(uint32_t& ones, uint32_t& twos, uint32
         : [t] "=&v"(t), [o] "+v"(ones), [w] "+v"(twos), [T] "+v"(T)
         : [a] "v"(a), [b] "v"(b), [sa] "v"(sa), [sb] "v"(sb));
 }
-// cell update, first pass for digit d:  U = cT|rT|bT, H = cH|rH|bH, c &= ~U | s (0xB0: S0 & (~S1 | S2)),
+// cell update, first pass for digit d:  U = cT|rT|bT, H = ~(cW & rW & bW) (0x7F; W = twos: a candidate of
+// the cell outside some unit's twos is that unit's hidden single), c &= ~U | s (0xB0: S0 & (~S1 | S2)),
 // anyh |= c & H (0xF8); with CHG, chg |= c_old & ~c_new (0xF4: S0 | S1 & ~S2)
 template <bool CHG>
 __device__ __forceinline__ void p32_upd1(uint32_t& c, uint32_t& H, uint32_t& anyh, uint32_t& chg, uint32_t s,
@@ -197,7 +204,7 @@ __device__ __forceinline__ void p32_upd1(uint32_t& c, uint32_t& H, uint32_t& any
     uint32_t U, v;
     if (CHG)
         asm("v_or3_b32 %[u], %[ct], %[rt], %[bt]\n\t"
-            "v_or3_b32 %[h], %[ch], %[rh], %[bh]\n\t"
+            "v_bitop3_b32 %[h], %[ch], %[rh], %[bh] bitop3:0x7f\n\t"
             "v_bitop3_b32 %[v], %[c], %[u], %[s] bitop3:0xb0\n\t"
             "v_bitop3_b32 %[g], %[g], %[c], %[v] bitop3:0xf4\n\t"
             "v_bitop3_b32 %[a], %[a], %[v], %[h] bitop3:0xf8"
@@ -206,7 +213,7 @@ __device__ __forceinline__ void p32_upd1(uint32_t& c, uint32_t& H, uint32_t& any
               [bh] "v"(bH));
     else
         asm("v_or3_b32 %[u], %[ct], %[rt], %[bt]\n\t"
-            "v_or3_b32 %[h], %[ch], %[rh], %[bh]\n\t"
+            "v_bitop3_b32 %[h], %[ch], %[rh], %[bh] bitop3:0x7f\n\t"
             "v_bitop3_b32 %[v], %[c], %[u], %[s] bitop3:0xb0\n\t"
             "v_bitop3_b32 %[a], %[a], %[v], %[h] bitop3:0xf8"
             : [u] "=&v"(U), [h] "=&v"(H), [v] "=&v"(v), [a] "+v"(anyh)
@@ -247,15 +254,15 @@ __device__ __forceinline__ void p32_unit_cells(uint32_t j, uint32_t& u0, uint32_
 
 // digits given twice in the lane's unit (a group's first step, before p32_unit: its closed cells are
 // the givens); such a board is not exact and goes to the search
-__device__ __forceinline__ uint32_t p32_dups(const P32Lane& w) {
-    uint32_t u0, ua, ub;
-    p32_unit_cells(p32_opq(w.hl), u0, ua, ub);
+__device__ __forceinline__ uint32_t p32_dups(const P32Lane& w, const p32_lds_t* lds) {
+    // the unit's cells from p32_unit's order table (any order will do; no lane-dependent branch)
+    const uint32_t tb = kP32Table + 40u * p32_opq(threadIdx.x);
     uint32_t T[9], dup = 0u;
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
-        const uint32_t o = u0 + (uint32_t)(q % 3) * ua + (uint32_t)(q / 3) * ub;
-        const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
-                    r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
+        const uint32_t o = *(const volatile __attribute__((address_space(3))) uint32_t*)(lds + tb + 4u * (q < 3 ? q : q + 1));
+        const uint2 r0 = p32_lda(o), r1 = p32_lda(o + 8), r2 = p32_lda(o + 16), r3 = p32_lda(o + 24),
+                    r4 = p32_lda(o + 32);
         const uint32_t a[9] = {r0.x, r0.y, r1.x, r1.y, r2.x, r2.y, r3.x, r3.y, r4.x};
 #pragma unroll
         for (int d = 0; d < 9; ++d) {
@@ -283,71 +290,18 @@ __device__ __forceinline__ uint32_t p32_dups(const P32Lane& w) {
 // were bank conflicts).  The per-lane offsets are a table in LDS (12 words per lane, 3 reads a step).
 __device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds, uint32_t& miss) {
     const uint32_t j = p32_opq(w.hl);   // the unit record written below
-    const __attribute__((address_space(3))) p32_u4* tb =
-        (const __attribute__((address_space(3))) p32_u4*)(lds + kP32Table + 48u * w.hl);
-    const p32_u4 ta = tb[0], tc = tb[1];
-    const uint32_t t8 = *(const __attribute__((address_space(3))) uint32_t*)(lds + kP32Table + 48u * w.hl + 32u);
-    const uint32_t ord[9] = {ta[0], ta[1], ta[2], ta[3], tc[0], tc[1], tc[2], tc[3], t8};
+    const uint32_t tb = kP32Table + 40u * p32_opq(threadIdx.x);
     uint32_t ones[9], twos[9], T[9];
-#if SDK_PROP32_UNIT_PAIR
-    // cells 0, 1 (ten fewer registers than three at a time), then pairs (2, 3) .. (6, 7), then cell 8
-    {
-        uint32_t a[2][9], s[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t o = u0 + (uint32_t)q * ua;
-            const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
-                        r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
-            a[q][0] = r0.x; a[q][1] = r0.y; a[q][2] = r1.x; a[q][3] = r1.y; a[q][4] = r2.x;
-            a[q][5] = r2.y; a[q][6] = r3.x; a[q][7] = r3.y; a[q][8] = r4.x;
-            s[q] = r4.y;
-        }
-#pragma unroll
-        for (int d = 0; d < 9; ++d) {
-            ones[d] = a[0][d] | a[1][d];
-            twos[d] = a[0][d] & a[1][d];
-            T[d] = (a[0][d] & s[0]) | (a[1][d] & s[1]);
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        asm volatile("" : "+v"(ones[0]), "+v"(ones[1]), "+v"(ones[2]), "+v"(ones[3]), "+v"(ones[4]), "+v"(ones[5]),
-                     "+v"(ones[6]), "+v"(ones[7]), "+v"(ones[8]), "+v"(twos[0]), "+v"(twos[1]), "+v"(twos[2]),
-                     "+v"(twos[3]), "+v"(twos[4]), "+v"(twos[5]), "+v"(twos[6]), "+v"(twos[7]), "+v"(twos[8]),
-                     "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]), "+v"(T[6]),
-                     "+v"(T[7]), "+v"(T[8])::"memory");
-        const int nq = p < 3 ? 2 : 1;
-        uint32_t a[2][9], s[2];
-#pragma unroll
-        for (int h = 0; h < nq; ++h) {
-            const int q = 2 + 2 * p + h;
-            const uint32_t o = u0 + (uint32_t)(q % 3) * ua + (uint32_t)(q / 3) * ub;
-            const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
-                        r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
-            a[h][0] = r0.x; a[h][1] = r0.y; a[h][2] = r1.x; a[h][3] = r1.y; a[h][4] = r2.x;
-            a[h][5] = r2.y; a[h][6] = r3.x; a[h][7] = r3.y; a[h][8] = r4.x;
-            s[h] = r4.y;
-        }
-#pragma unroll
-        for (int d = 0; d < 9; ++d) {
-            if (nq == 2) {
-                p32_unit2(ones[d], twos[d], T[d], a[0][d], a[1][d], s[0], s[1]);
-            } else {
-                twos[d] |= ones[d] & a[0][d];
-                ones[d] |= a[0][d];
-                T[d] |= a[0][d] & s[0];
-            }
-        }
-    }
-#else
     // cells 0, 1, 2
     {
         uint32_t a[3][9], s[3];
+        const uint64_t o01 = *(const volatile __attribute__((address_space(3))) uint64_t*)(lds + tb);
+        const uint32_t o2 = *(const volatile __attribute__((address_space(3))) uint32_t*)(lds + tb + 8u);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            const uint32_t o = ord[q];
-            const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
-                        r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
+            const uint32_t o = q == 0 ? (uint32_t)o01 : q == 1 ? (uint32_t)(o01 >> 32) : o2;
+            const uint2 r0 = p32_lda(o), r1 = p32_lda(o + 8), r2 = p32_lda(o + 16), r3 = p32_lda(o + 24),
+                        r4 = p32_lda(o + 32);
             a[q][0] = r0.x; a[q][1] = r0.y; a[q][2] = r1.x; a[q][3] = r1.y; a[q][4] = r2.x;
             a[q][5] = r2.y; a[q][6] = r3.x; a[q][7] = r3.y; a[q][8] = r4.x;
             s[q] = r4.y;
@@ -368,12 +322,12 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds,
                      "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]), "+v"(T[6]),
                      "+v"(T[7]), "+v"(T[8])::"memory");
         uint32_t a[2][9], s[2];
+        const uint64_t op = *(const volatile __attribute__((address_space(3))) uint64_t*)(lds + tb + 16u + 8u * p);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int q = 3 + 2 * p + h;
-            const uint32_t o = ord[q];
-            const uint2 r0 = p32_ld(w.reg, o), r1 = p32_ld(w.reg, o + 8), r2 = p32_ld(w.reg, o + 16),
-                        r3 = p32_ld(w.reg, o + 24), r4 = p32_ld(w.reg, o + 32);
+            const uint32_t o = h == 0 ? (uint32_t)op : (uint32_t)(op >> 32);
+            const uint2 r0 = p32_lda(o), r1 = p32_lda(o + 8), r2 = p32_lda(o + 16), r3 = p32_lda(o + 24),
+                        r4 = p32_lda(o + 32);
             a[h][0] = r0.x; a[h][1] = r0.y; a[h][2] = r1.x; a[h][3] = r1.y; a[h][4] = r2.x;
             a[h][5] = r2.y; a[h][6] = r3.x; a[h][7] = r3.y; a[h][8] = r4.x;
             s[h] = r4.y;
@@ -383,14 +337,20 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds,
             p32_unit2(ones[d], twos[d], T[d], a[0][d], a[1][d], s[0], s[1]);
         }
     }
-#endif
-    miss = 0u;
-#pragma unroll
-    for (int d = 0; d < 9; ++d) miss |= ~ones[d];
+    // a digit with no cell: the complement of the and of the nine "in some cell" words (and3 chains)
+    uint32_t all;
+    asm("v_bitop3_b32 %[m], %[o0], %[o1], %[o2] bitop3:0x80\n\t"
+        "v_bitop3_b32 %[m], %[m], %[o3], %[o4] bitop3:0x80\n\t"
+        "v_bitop3_b32 %[m], %[m], %[o5], %[o6] bitop3:0x80\n\t"
+        "v_bitop3_b32 %[m], %[m], %[o7], %[o8] bitop3:0x80"
+        : [m] "=&v"(all)
+        : [o0] "v"(ones[0]), [o1] "v"(ones[1]), [o2] "v"(ones[2]), [o3] "v"(ones[3]), [o4] "v"(ones[4]),
+          [o5] "v"(ones[5]), [o6] "v"(ones[6]), [o7] "v"(ones[7]), [o8] "v"(ones[8]));
+    miss = ~all;
     __builtin_amdgcn_wave_barrier();   // every lane's reads before the records are overwritten
     const uint32_t urec = kP32URec * j;   // spare lanes: unit slots 27..31
 #pragma unroll
-    for (int d = 0; d < 9; ++d) p32_st(w.reg, urec + 8 * d, T[d], ones[d] & ~twos[d]);
+    for (int d = 0; d < 9; ++d) p32_st(w.reg, urec + 8 * d, T[d], twos[d]);
 }
 
 __device__ __forceinline__ uint32_t w_rowrec(uint32_t base, int k) { return base + 216u * (uint32_t)k; }
@@ -616,10 +576,6 @@ __device__ __forceinline__ uint32_t p32_dequeue(const Prop32Args& a, uint32_t gr
     return ~0u;
 }
 
-#ifndef SDK_PROP32_UNIT_PAIR
-#define SDK_PROP32_UNIT_PAIR 0
-#endif
-
 // SDK_PROP32_STATS (profiling builds only): per group, histograms of the steps it ran, of the step at
 // which at most 4 / at most 1 of its boards were still live, and the locked-candidates passes
 #ifndef SDK_PROP32_STATS
@@ -657,18 +613,21 @@ __constant__ uint8_t kP32Order[81] = {2, 5, 8, 1, 4, 7, 3, 0, 6, 1, 4, 7, 0, 3, 
                                       2, 7, 4, 1, 5, 8, 2, 4, 7, 1, 6, 3, 0, 4, 7, 1, 3, 6, 0, 5, 2, 8, 3, 6, 0,
                                       2, 5, 8, 4, 1, 7};
 
-// p32_unit's per-lane read order, lane j at kP32Table + 48 j: word t = the record offset of the cell
-// of unit j whose kP32Order entry is t.  Spare lanes take lane 0's (one more reader of each address).
-// Written once per workgroup.
+// p32_unit's per-lane read order, lane L (half L / 32, unit L % 32) at kP32Table + 40 L: word t = the
+// LDS address of the cell of the unit whose kP32Order entry is t, in the lane's half (no per-read
+// address add).  Spare lanes take unit 0's (one more reader of each address).  Written once per
+// workgroup.
 __device__ __forceinline__ void p32_order_table(p32_lds_t* lds) {
-    if (threadIdx.x >= 32) return;
+    const uint32_t hl = threadIdx.x & 31u;
     uint32_t u0, ua, ub;
-    p32_unit_cells(threadIdx.x < 27 ? threadIdx.x : 0u, u0, ua, ub);
+    p32_unit_cells(hl < 27 ? hl : 0u, u0, ua, ub);
     __attribute__((address_space(3))) uint32_t* tab =
-        (__attribute__((address_space(3))) uint32_t*)(lds + kP32Table + 48u * threadIdx.x);
+        (__attribute__((address_space(3))) uint32_t*)(lds + kP32Table + 40u * threadIdx.x);
+    const uint32_t region = (uint32_t)(uintptr_t)lds + (threadIdx.x >> 5) * kP32Region;
     for (uint32_t q = 0; q < 9; ++q) {
         const uint32_t o = u0 + (q % 3) * ua + (q / 3) * ub;
-        tab[kP32Order[o / kP32Rec]] = o;
+        const uint32_t t = kP32Order[o / kP32Rec];
+        tab[t < 3u ? t : t + 1u] = region + o;   // words 0-2, then the pairs (3, 4) .. (7, 8) 8-byte aligned
     }
 }
 
@@ -748,7 +707,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         uint32_t st_lc = 0, st_t4 = ~0u, st_t1 = ~0u;
 #endif
         uint32_t it = 0;
-        for (;;) {
+        // One exit, at the head: a group that ends in a step still runs that step's cells phase (sound
+        // propagation; it only tightens what a handed-over board carries), so every path through the
+        // body ends in an update of the cell words and they keep one register home (with exits in the
+        // middle of the step the register allocator gave the words a second home and copied all 27
+        // out and back on every step)
+        while (live != 0ull) {
             uint32_t empty, alls;
             p32_singles(w, x, empty, alls);
             __builtin_amdgcn_wave_barrier();
@@ -763,12 +727,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
                 live &= ~stuck;
                 fixw = 0ull;
                 lc = false;
-                if (live == 0ull) break;
                 __builtin_amdgcn_wave_barrier();
                 continue;
             }
             if (it == 0) {   // a digit given twice: not exact, to the search
-                const uint32_t dup = p32_dups(w);
+                const uint32_t dup = p32_dups(w, lds);
                 const uint64_t dupw = p32_mask64(p32_half_or(w.act ? dup : 0u)) & live;
                 undec |= dupw;
                 inexact |= dupw;
@@ -786,19 +749,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
             if (st_t4 == ~0u && __builtin_popcountll(live) <= 4) st_t4 = it;
             if (st_t1 == ~0u && __builtin_popcountll(live) <= 1) st_t1 = it;
 #endif
-            if (live == 0ull) break;
-            if (a.tail_live && it >= a.tail_step && (uint32_t)__builtin_popcountll(live) <= a.tail_live) {
-                undec |= live;   // the last few boards go to the search with their propagated grids
-                break;
-            }
-            if (++it >= a.max_steps) {
-                undec |= live;
-                break;
+            if (live != 0ull) {
+                if (a.tail_live && it >= a.tail_step && (uint32_t)__builtin_popcountll(live) <= a.tail_live) {
+                    undec |= live;   // the last few boards go to the search with their propagated grids
+                    live = 0ull;
+                } else if (++it >= a.max_steps) {
+                    undec |= live;
+                    live = 0ull;
+                }
             }
             __builtin_amdgcn_wave_barrier();
             // every lc_every-th step is followed by a locked-candidates pass; that step also reports
             // which boards it left unchanged (a board unchanged by it and by the pass is stuck)
-            lc = (it % a.lc_every) == 0u;
+            lc = live != 0ull && (it % a.lc_every) == 0u;
             if (lc) {
                 const uint32_t chg_own = p32_cells<true>(w, x);
                 fixw = live & ~p32_mask64(p32_half_or(w.act ? chg_own : 0u));
@@ -826,7 +789,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
             uint32_t empty, alls;
             p32_singles(w, x, empty, alls);
             __builtin_amdgcn_wave_barrier();
-            const uint64_t dupw = p32_mask64(p32_half_or(w.act ? p32_dups(w) : 0u)) & handed;
+            const uint64_t dupw = p32_mask64(p32_half_or(w.act ? p32_dups(w, lds) : 0u)) & handed;
             contra |= dupw;
             undec &= ~dupw;
             handed &= ~dupw;

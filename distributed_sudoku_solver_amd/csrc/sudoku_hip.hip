@@ -844,8 +844,8 @@ int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t*
                       static_cast<int8_t*>(c->p32_st.p), nullptr, n, 0, 0, nullptr, nullptr, 0, 1, order, budget,
                       donate, lst);
     if (!rc) {
-        // one thread per byte of the list's boards (its length is on the device: sized for all n)
-        const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n * 81 + 255) / 256, (uint64_t)c->cus * 8));
+        // one thread per 4 bytes of the list's boards (its length is on the device: sized for all n)
+        const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n * 81 + 1023) / 1024, (uint64_t)c->cus * 8));
         if (sdk::launch_p32_scatter(lst, static_cast<uint8_t*>(c->p32_out.p), static_cast<int8_t*>(c->p32_st.p), d_in,
                                     d_out, d_status, g, c->stream) != hipSuccess)
             rc = fail(SDK_EHIP, "prop32 scatter launch failed");

@@ -54,9 +54,6 @@ namespace sdk {
 #ifndef SDK_SOLVE4_LDS_LEVELS
 #define SDK_SOLVE4_LDS_LEVELS 0
 #endif
-#ifndef SDK_SOLVE4_EXACT_UPD
-#define SDK_SOLVE4_EXACT_UPD 1        // exact waves also drop the two-hidden-singles test (upd4x)
-#endif
 #ifndef SDK_SOLVE4_TAIL_DIV
 #define SDK_SOLVE4_TAIL_DIV 128       // the shared dequeue tail: n / this boards (32 to round 3: profiles/r03/ab_tail_size2.log)
 #endif
@@ -365,17 +362,11 @@ __device__ __forceinline__ void unit4(const uint2 (&v)[9], uint32_t E, uint32_t 
 // carries E = kFresh4 in its half; a round of a wave with such a board reads the same nine cell
 // words a statics pass would -- at the first round a board's closed cells are exactly its givens --
 // and derives D and E from them (unit4f) before they are used.
-#ifndef SDK_SOLVE4_FRESH_ROUND
-#define SDK_SOLVE4_FRESH_ROUND 1   // round 4: +1.9 % on 10M 17-clue (4 A/B pairs), the rest within noise
-#endif
 constexpr uint32_t kFresh4 = 0x8000u;                 // E of a board whose statics are pending
 // the plain kernel only: the donation kernel keeps statics4 (its 96-VGPR build spills a 64-bit
 // value to an odd register pair with unit4f, which the gfx950 backend rejects)
-constexpr bool kFresh4Round = SDK_SOLVE4_FRESH_ROUND != 0;
+constexpr bool kFresh4Round = true;   // round 4: +1.9 % on 10M 17-clue (4 A/B pairs), the rest within noise
 
-#ifndef SDK_SOLVE4_SPLIT_READS
-#define SDK_SOLVE4_SPLIT_READS 1
-#endif
 
 // unit4 for a round of a wave where some board just started (its E half = kFresh4): that
 // board's statics come from the nine cells read here (its closed cells are its givens):
@@ -499,7 +490,6 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bad,
     wave_sync();
     uint32_t m0, m1, m2;
     chg = 0;
-#if SDK_SOLVE4_SPLIT_READS
     // The seven unit reads as single ds_read_b64s: left to itself the compiler pairs
     // them into ds_read2_b64, which takes 8 LDS-array cycles per wave-instruction
     // against 2 x 2 for two ds_read_b64 (MI355X_MICROARCH.md, LDS table).  Issued in
@@ -521,22 +511,14 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bad,
         : "memory");
     asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(uc), "+v"(r0), "+v"(b0)::"memory");
     const uint32_t ucx = (uint32_t)uc, ucy = (uint32_t)(uc >> 32);
-    ((EXACT && SDK_SOLVE4_EXACT_UPD) ? upd4x : upd4)(c.x0, c.s0, ucx | (uint32_t)r0 | (uint32_t)b0, ucy | (uint32_t)(r0 >> 32) | (uint32_t)(b0 >> 32), bm, m0,
+    (EXACT ? upd4x : upd4)(c.x0, c.s0, ucx | (uint32_t)r0 | (uint32_t)b0, ucy | (uint32_t)(r0 >> 32) | (uint32_t)(b0 >> 32), bm, m0,
          chg);
     asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(r1), "+v"(b1), "+v"(c.x0), "+v"(c.s0)::"memory");
-    ((EXACT && SDK_SOLVE4_EXACT_UPD) ? upd4x : upd4)(c.x1, c.s1, ucx | (uint32_t)r1 | (uint32_t)b1, ucy | (uint32_t)(r1 >> 32) | (uint32_t)(b1 >> 32), bm, m1,
+    (EXACT ? upd4x : upd4)(c.x1, c.s1, ucx | (uint32_t)r1 | (uint32_t)b1, ucy | (uint32_t)(r1 >> 32) | (uint32_t)(b1 >> 32), bm, m1,
          chg);
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r2), "+v"(b2), "+v"(c.x1), "+v"(c.s1)::"memory");
-    ((EXACT && SDK_SOLVE4_EXACT_UPD) ? upd4x : upd4)(c.x2, c.s2, ucx | (uint32_t)r2 | (uint32_t)b2, ucy | (uint32_t)(r2 >> 32) | (uint32_t)(b2 >> 32), bm, m2,
+    (EXACT ? upd4x : upd4)(c.x2, c.s2, ucx | (uint32_t)r2 | (uint32_t)b2, ucy | (uint32_t)(r2 >> 32) | (uint32_t)(b2 >> 32), bm, m2,
          chg);
-#else
-    const uint2 uc = w.s_unit[w.ucol];
-    const uint2 r0 = w.s_unit[w.ur0], r1 = w.s_unit[w.ur0 + 3], r2 = w.s_unit[w.ur0 + 6];
-    const uint2 b0 = w.s_unit[w.ub0], b1 = w.s_unit[w.ub0 + 3], b2 = w.s_unit[w.ub0 + 6];
-    upd4(c.x0, c.s0, uc.x | r0.x | b0.x, uc.y | r0.y | b0.y, bm, m0, chg);
-    upd4(c.x1, c.s1, uc.x | r1.x | b1.x, uc.y | r1.y | b1.y, bm, m1, chg);
-    upd4(c.x2, c.s2, uc.x | r2.x | b2.x, uc.y | r2.y | b2.y, bm, m2, chg);
-#endif
     // an open cell without candidates (a zero half of m0..m2); exact waves leave it to the
     // missing-digit test (upd4x)
     bad = EXACT ? bm : bm | z16(min16(min16(m0, m1), m2));
@@ -684,13 +666,10 @@ struct DnCtl {
     DnSeed seed;              // own cache line: idle waves take seed items at the launch's start
 };
 constexpr uint32_t kDnErrReg = 1u, kDnErrLock = 2u, kDnErrSeed = 4u;
-// ticket reservation (SDK_DN_CAS): 2 (default) an add, then the tickets past reg_tail handed back
-// by one compare-and-swap; 1 a compare-and-swap loop (never passes reg_tail, but under
-// contention most donation checks fail: 1,300 instead of 1,765 items on the heavy-1000 launch,
-// 1.25 vs 1.08 ms); 0 round 3's add alone.  SDK_DN_ERRCHECK=0: no error-word read (measurement)
-#ifndef SDK_DN_CAS
-#define SDK_DN_CAS 2
-#endif
+// ticket reservation: an add, then the tickets past reg_tail handed back by one compare-and-swap
+// (round 4 A/B, profiles/r04 via tools/gpu_r04j.sh: a compare-and-swap loop never passes reg_tail,
+// but under contention most donation checks fail -- 1,300 instead of 1,765 items on the heavy-1000
+// launch, 1.25 vs 1.08 ms).  SDK_DN_ERRCHECK=0: no error-word read (measurement)
 #ifndef SDK_DN_ERRCHECK
 #define SDK_DN_ERRCHECK 1
 #endif
@@ -934,31 +913,12 @@ __device__ __forceinline__ void dn_donate4(const Lane4& w, const Args4& a, const
     // another donor took tickets in between -- then those registrations stay unserved (a
     // wave left idle until the launch ends: throughput, never an answer or termination)
     uint32_t t0 = 0, valid = 0;
-#if SDK_DN_CAS != 1   // 0: round 3's reservation (a stale head can pass reg_tail); 2: the same,
-                     // then the tickets past reg_tail handed back by one compare-and-swap
     if (w.hl == 0) {
         const uint32_t want = min(cnt, tail - head);
         t0 = atomicAdd(&ctl->x[x].reg_head, want);
         const uint32_t tail2 = min(ld_agent(&ctl->x[x].reg_tail), kDnRegX);
         valid = tail2 > t0 ? min(want, tail2 - t0) : 0u;
-        if (SDK_DN_CAS == 2 && valid < want) atomicCAS(&ctl->x[x].reg_head, t0 + want, t0 + valid);
-    }
-    if (false) {
-#else
-    if (w.hl == 0 && cnt != 0u) {
-#endif
-        uint32_t h = head, t = min(tail, kDnRegX);
-        for (int it = 0; it < 8 && t > h; ++it) {
-            const uint32_t want = min(cnt, t - h);
-            const uint32_t old = atomicCAS(&ctl->x[x].reg_head, h, h + want);
-            if (old == h) {
-                t0 = h;
-                valid = want;
-                break;
-            }
-            h = old;
-            t = min(ld_agent(&ctl->x[x].reg_tail), kDnRegX);
-        }
+        if (valid < want) atomicCAS(&ctl->x[x].reg_head, t0 + want, t0 + valid);
     }
     // a bounded wait ran out: no more donation (the error word is read only by a donor that
     // holds tickets -- in every donation check it cost the heavy-1000 launch ~15 %: the
@@ -1435,24 +1395,8 @@ __device__ __forceinline__ void statics4(const Lane4& w, Cells4& c) {
 
 template <int HI, bool FR = false>
 __device__ __forceinline__ void next_board4(const Lane4& w, const Lane4& wr, const Args4& a, Slot4& b, Cells4& c) {
-#if SDK_SOLVE4_STATIC == 1   // experiment: boards dealt round robin to the slots, no dequeue atomics
-    b.bidx = b.bend == 0u ? blockIdx.x * 4u + (uint32_t)w.half * 2u + HI : b.bidx + gridDim.x * 4u;
-    b.bend = 1u;
-    if (false) {
-#elif SDK_SOLVE4_STATIC == 2   // experiment: one contiguous block of boards per slot, no atomics
-    if (b.bend == 0u) {
-        const uint64_t S = (uint64_t)gridDim.x * 4u, s = blockIdx.x * 4u + (uint32_t)w.half * 2u + HI;
-        b.bidx = (uint32_t)(a.n * s / S);
-        b.bend = (uint32_t)(a.n * (s + 1) / S);
-        if (b.bidx >= b.bend) b.bidx = (uint32_t)a.n;
-    } else if (++b.bidx >= b.bend) {
-        b.bidx = (uint32_t)a.n;
-    }
-    if (false) {
-#else
     ++b.bidx;
     if (b.bidx >= b.bend) {
-#endif
         if (a.heads) {
             // XCD-local segment (see kHeads), then the shared tail: straight-line code, no
             // segment-walking loop (its control flow alone made the allocator spill the
@@ -1973,7 +1917,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DN ? SDK_SOL
         // every board of the wave exact (an inactive slot is not): the shorter round
         if (a.locked && __builtin_amdgcn_ballot_w64(c.E != kC2) == 0)
             PROF4(0, round4<true>(w, c, badw, chg));
-        else   // SDK_SOLVE4_FRESH_ROUND: also the rounds of waves with a board that just started
+        else   // kFresh4Round: also the rounds of waves with a board that just started
             PROF4(0, (round4<false, kFresh4Round && !DN>(w, c, badw, chg)));
         ++a.iter;
         const uint64_t B0 = spread_halves(__builtin_amdgcn_ballot_w64((badw & 0xFFFFu) != 0u));

@@ -91,6 +91,8 @@ def parse_args():
                          "1000 heaviest, one launch vs the phased solve with subtree donation (0 = skip)")
     ap.add_argument("--hard-reps", type=int, default=10, help="hard_1m: symmetries of the 100k hard set per GPU")
     ap.add_argument("--prop32", type=int, default=-1, help="SDK_OPT_PROP32 for every leg (-1 = library default)")
+    ap.add_argument("--hard-split-inflight", type=int, default=0,
+                    help="hard legs: split budget of the donation_in_flight mode (0 = the library's rule)")
     ap.add_argument("--opt", action="append", default=[],
                     help="NAME=VALUE: an SDK_OPT_* engine option for every leg (experiments), e.g. PROP32_LC=3")
     ap.add_argument("--hard-inflight", type=int, default=3,
@@ -540,7 +542,8 @@ def hard_leg(eng, d, args, synth, L):
                                      ("donation", L.SDK_ORDER_LEX, split_dn.get(name, 1), 1),
                                      ("mrv_one_launch", L.SDK_ORDER_MRV_UNIQUE, 0, 1),
                                      ("mrv_donation", L.SDK_ORDER_MRV_UNIQUE, split_dn.get(name, 1), 1),
-                                     ("donation_in_flight", L.SDK_ORDER_LEX, split_dn.get(name, 1),
+                                     ("donation_in_flight", L.SDK_ORDER_LEX,
+                                      args.hard_split_inflight or split_dn.get(name, 1),
                                       args.hard_inflight or args.inflight)):
             if ctx < 2 and mode == "donation_in_flight":
                 continue

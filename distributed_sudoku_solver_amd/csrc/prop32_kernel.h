@@ -13,9 +13,11 @@
 // every board is decided here (tools/lockstep_model.py: all of 2,048 solved by propagation).
 //
 // Layout.  Bit b of a 32-bit word is board b of the half's group of 32 (board base + 32 * half + b).
-// Lane hl < 27 of a half owns cells hl, hl + 27, hl + 54 -- as in solve4 -- with nine candidate
-// words per cell (c[k][d], bit b set: digit d + 1 is still possible in that cell of board b) and
-// unit hl (rows 0-8, columns 9-17, boxes 18-26).  A cell is closed when exactly one candidate is
+// Lane hl < 27 of a half owns row triad hl -- cells 3 hl .. 3 hl + 2, one row, one box -- with nine
+// candidate words per cell (c[k][d], bit b set: digit d + 1 is still possible in that cell of board
+// b) and unit hl (rows 0-8, columns 9-17, boxes 18-26).  A triad's cells share their row and box, so
+// the cell update reads five unit records, not seven, and the locked-candidates pass has the
+// presence and eliminations of the lane's own row triad in registers.  A cell is closed when exactly one candidate is
 // left (its single word s[k]); no separate closed state.  Lanes 27..31 run the same code on spare
 // slots (their results are masked out).
 //
@@ -129,7 +131,7 @@ struct P32Cells {
 };
 
 // singles: s = exactly one candidate, empty = none; the cell records of the real lanes (cell j at
-// 40j: cells hl + 27k at 40 hl + 1080k)
+// 40j: cells 3 hl + k at 120 hl + 40k)
 __device__ __forceinline__ void p32_singles(const P32Lane& w, P32Cells& x, uint32_t& empty, uint32_t& alls) {
     empty = 0u;
     alls = ~0u;
@@ -160,7 +162,7 @@ __device__ __forceinline__ void p32_singles(const P32Lane& w, P32Cells& x, uint3
     const uint32_t rec = kP32Rec * p32_opq(w.hl);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const uint32_t o = w.act ? rec + 1080u * k : 81u * kP32Rec;
+        const uint32_t o = w.act ? 3u * rec + kP32Rec * k : 81u * kP32Rec;
         p32_st(w.reg, o, x.c[k][0], x.c[k][1]);
         p32_st(w.reg, o + 8, x.c[k][2], x.c[k][3]);
         p32_st(w.reg, o + 16, x.c[k][4], x.c[k][5]);
@@ -353,21 +355,24 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds,
     for (int d = 0; d < 9; ++d) p32_st(w.reg, urec + 8 * d, T[d], twos[d]);
 }
 
-__device__ __forceinline__ uint32_t w_rowrec(uint32_t base, int k) { return base + 216u * (uint32_t)k; }
-
 // the cell update of one step; CHG: also returns the change bits of the lane's three cells (only the
-// step before a locked-candidates pass needs them: a board unchanged by it and by the pass is stuck)
+// step before a locked-candidates pass needs them: a board unchanged by it and by the pass is stuck).
+// The lane's cells 3j + k share row j / 3 and box 3 (j / 9) + j % 3: those two records are read once
+// (36 registers for the phase), each cell's column record beside its update.
 template <bool CHG>
 __device__ __forceinline__ uint32_t p32_cells(const P32Lane& w, P32Cells& x) {
     const uint32_t j = p32_opq(w.hl);
-    const uint32_t r0 = j / 9, col = j - 9 * r0;      // cells j + 27k: row r0 + 3k, column col
-    const uint32_t colrec = kP32URec * (9 + col), rowrec = kP32URec * r0, boxrec = kP32URec * (18 + col / 3);
-    uint32_t cT[9], cH[9];
+    const uint32_t r = j / 3, bc = j - 3 * r;          // row r, box column bc: columns 3 bc + k
+    const uint32_t rowrec = kP32URec * r, boxrec = kP32URec * (18 + 3 * (r / 3) + bc),
+                   colrec = kP32URec * (9 + 3 * bc);
+    uint32_t rT[9], rW[9], bT[9], bW[9];
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
-        const uint2 v = p32_ld(w.reg, colrec + 8 * d);
-        cT[d] = v.x;
-        cH[d] = v.y;
+        const uint2 v = p32_ld(w.reg, rowrec + 8 * d), u = p32_ld(w.reg, boxrec + 8 * d);
+        rT[d] = v.x;
+        rW[d] = v.y;
+        bT[d] = u.x;
+        bW[d] = u.y;
     }
     uint32_t chg = 0u;
 #pragma unroll
@@ -375,9 +380,8 @@ __device__ __forceinline__ uint32_t p32_cells(const P32Lane& w, P32Cells& x) {
         uint32_t H[9], anyh = 0u;
 #pragma unroll
         for (int d = 0; d < 9; ++d) {
-            const uint2 r = p32_ld(w.reg, w_rowrec(rowrec, k) + 8 * d);   // row r0 + 3k
-            const uint2 b = p32_ld(w.reg, w_rowrec(boxrec, k) + 8 * d);   // box 3k + col / 3
-            p32_upd1<CHG>(x.c[k][d], H[d], anyh, chg, x.s[k], cT[d], r.x, b.x, cH[d], r.y, b.y);
+            const uint2 c = p32_ld(w.reg, colrec + kP32URec * k + 8 * d);   // column 3 bc + k
+            p32_upd1<CHG>(x.c[k][d], H[d], anyh, chg, x.s[k], c.x, rT[d], bT[d], c.y, rW[d], bW[d]);
         }
 #pragma unroll
         for (int d = 0; d < 9; ++d) p32_upd2<CHG>(x.c[k][d], H[d], anyh, chg);
@@ -411,27 +415,24 @@ __device__ __forceinline__ void p32_elim(const P32Lane& w, uint32_t tl, uint32_t
 }
 
 // one locked-candidates pass (the cell records of this step are in LDS); returns the change bits.
-// Lane j < 27 owns row triad j (row j / 3, box column j % 3) and column triad j (column j / 3,
-// box row j % 3); spare lanes read triad 26's cells and write their own slots 27..31.
+// Lane j < 27 owns row triad j (row j / 3, box column j % 3) -- its own three cells -- and column
+// triad j (column j / 3, box row j % 3); spare lanes read triad 26's column and write their own
+// slots 27..31.
 __device__ __forceinline__ uint32_t p32_locked(const P32Lane& w, P32Cells& x) {
     const uint32_t j = p32_opq(w.hl), jt = min(j, 26u);
     const uint32_t tl = jt / 3, tb = jt - 3 * tl;
-    const uint32_t rtri = kP32Rec * (9 * tl + 3 * tb), ctri = kP32Rec * (27 * tb + tl);
+    const uint32_t ctri = kP32Rec * (27 * tb + tl);
     const uint32_t rtrec = kP32TRec * j, ctrec = kP32ColTri + kP32TRec * j;
-    // presence of the lane's row triad and column triad
+    // presence of the lane's row triad (its own cells, closed ones included) and column triad
     uint32_t pr[9], pc[9];
 #pragma unroll
+    for (int d = 0; d < 9; ++d) pr[d] = x.c[0][d] | x.c[1][d] | x.c[2][d];
+#pragma unroll
     for (int h = 0; h < 5; ++h) {
-        const uint2 a0 = p32_ld(w.reg, rtri + 8 * h), a1 = p32_ld(w.reg, rtri + 40 + 8 * h),
-                    a2 = p32_ld(w.reg, rtri + 80 + 8 * h);
         const uint2 b0 = p32_ld(w.reg, ctri + 8 * h), b1 = p32_ld(w.reg, ctri + 360 + 8 * h),
                     b2 = p32_ld(w.reg, ctri + 720 + 8 * h);
-        pr[2 * h] = a0.x | a1.x | a2.x;
         pc[2 * h] = b0.x | b1.x | b2.x;
-        if (h < 4) {
-            pr[2 * h + 1] = a0.y | a1.y | a2.y;
-            pc[2 * h + 1] = b0.y | b1.y | b2.y;
-        }
+        if (h < 4) pc[2 * h + 1] = b0.y | b1.y | b2.y;
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -444,30 +445,26 @@ __device__ __forceinline__ uint32_t p32_locked(const P32Lane& w, P32Cells& x) {
     p32_elim(w, tl, tb, 0u, er);
     p32_elim(w, tl, tb, kP32ColTri, ec);
     __builtin_amdgcn_wave_barrier();
+    // the column triads' eliminations to LDS (the row triad's are this lane's own cells')
 #pragma unroll
-    for (int h = 0; h < 5; ++h) {
-        p32_st(w.reg, rtrec + 8 * h, er[2 * h], h < 4 ? er[2 * h + 1] : 0u);
-        p32_st(w.reg, ctrec + 8 * h, ec[2 * h], h < 4 ? ec[2 * h + 1] : 0u);
-    }
+    for (int h = 0; h < 5; ++h) p32_st(w.reg, ctrec + 8 * h, ec[2 * h], h < 4 ? ec[2 * h + 1] : 0u);
     __builtin_amdgcn_wave_barrier();
-    // apply to the lane's open cells: cell j + 27k lies in row triad 3 (r0 + 3k) + col / 3 and
-    // column triad 3 col + k
-    const uint32_t r0 = j / 9, col = j - 9 * r0;
-    const uint32_t at_r = kP32TRec * (3 * r0 + col / 3), at_c = kP32ColTri + kP32TRec * (3 * col);
+    // apply to the lane's open cells: cell 3j + k lies in column 3 (j % 3) + k, box row j / 9, so in
+    // column triad 9 (j % 3) + 3k + j / 9
+    const uint32_t at_c = kP32ColTri + kP32TRec * (9 * (j % 3) + j / 9);
     uint32_t chg = 0u;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
 #pragma unroll
         for (int h = 0; h < 5; ++h) {
-            const uint2 r = p32_ld(w.reg, at_r + 360u * k + 8 * h);
-            const uint2 c = p32_ld(w.reg, at_c + 40u * k + 8 * h);
+            const uint2 c = p32_ld(w.reg, at_c + 3 * kP32TRec * k + 8 * h);
             {
-                const uint32_t rm = (r.x | c.x) & x.c[k][2 * h] & ~x.s[k];
+                const uint32_t rm = (er[2 * h] | c.x) & x.c[k][2 * h] & ~x.s[k];
                 chg |= rm;
                 x.c[k][2 * h] ^= rm;
             }
             if (h < 4) {
-                const uint32_t rm = (r.y | c.y) & x.c[k][2 * h + 1] & ~x.s[k];
+                const uint32_t rm = (er[2 * h + 1] | c.y) & x.c[k][2 * h + 1] & ~x.s[k];
                 chg |= rm;
                 x.c[k][2 * h + 1] ^= rm;
             }
@@ -708,7 +705,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         // undecided; their words do not matter)
         P32Cells x;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) p32_convert(w.reg + w.hl + 27u * k, x.c[k]);
+        for (int k = 0; k < 3; ++k) p32_convert(w.reg + 3u * w.hl + k, x.c[k]);
         // per-group bookkeeping as 64-bit board masks in scalar registers (bit 32h + b: board b of
         // half h)
         const uint64_t valid = nb >= 64u ? ~0ull : ((1ull << nb) - 1ull);
@@ -809,7 +806,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         }
         if ((solved | handed) && w.act) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) p32_digits(x.c[k], x.s[k], w.reg + w.hl + 27u * k);
+            for (int k = 0; k < 3; ++k) p32_digits(x.c[k], x.s[k], w.reg + 3u * w.hl + k);
         }
         for (uint64_t m = contra; m; m &= m - 1ull) {     // rare: the 81 bytes by 64 lanes
             const uint32_t p = (uint32_t)__builtin_ctzll(m);

@@ -67,7 +67,7 @@ def parse_args():
     ap.add_argument("--batch", type=int, default=10_000_000, help="C4 puzzles, whole job (sharded over the GPUs)")
     ap.add_argument("--weak-leg", type=int, default=1, help="N > 1: also time --batch puzzles per GPU (weak scaling)")
     ap.add_argument("--check-boards", type=int, default=100_000_000, help="checker boards per GPU (0 = skip)")
-    ap.add_argument("--check-steps", type=int, default=10)
+    ap.add_argument("--check-steps", type=int, default=20)
     ap.add_argument("--check-warmup", type=int, default=10,
                     help="untimed checker launches first (the memory clocks ramp under sustained streaming)")
     ap.add_argument("--order", choices=["mrv_unique", "lex"], default="lex")

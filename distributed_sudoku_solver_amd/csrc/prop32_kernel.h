@@ -695,8 +695,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         uint64_t inert64 = 0ull;
         if (hi_given) {
             bool bad = false;
-            if (threadIdx.x < nb) {
-                const p32_lds_t* row = lds + (threadIdx.x >> 5) * kP32Region + (threadIdx.x & 31u) * 81u;
+            const uint32_t t = p32_opq(threadIdx.x);   // (per-lane values recomputed per group: hoisted
+            if (t < nb) {                               // out of the group loop they were spilled)
+                const p32_lds_t* row = lds + (t >> 5) * kP32Region + (t & 31u) * 81u;
                 for (uint32_t c = 0; c < 81u; ++c) bad |= row[c] > 9u;
             }
             inert64 = __builtin_amdgcn_ballot_w64(bad);
@@ -836,7 +837,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
             }
         }
         // statuses; the undecided boards are listed with their inputs for the search
-        const uint32_t me = threadIdx.x;                  // board me of the group (32 half + hl)
+        const uint32_t me = p32_opq(threadIdx.x);        // board me of the group (32 half + hl)
         if ((valid >> me) & 1ull)
             a.status[base + me] = (int8_t)(((solved >> me) & 1ull) ? 1 : (((contra >> me) & 1ull) ? 0 : kStUndecided));
         if (undec) {

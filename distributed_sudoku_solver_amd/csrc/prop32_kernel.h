@@ -8,8 +8,9 @@
 // and the input grid back (DHT_Node.py:535).  Everything else -- a board propagation leaves open,
 // a board with a duplicated or out-of-domain given (whose units are not "exact", see solve4_kernel.h
 // unit4x), a board still changing after max_steps -- is left undecided (kStUndecided): it goes to
-// the fallback list with its input, solve4_kernel searches it from scratch, and its answer is
-// scattered back (sudoku_hip.hip, launch_solve).  On the 17-clue workload of the headline metric
+// the fallback list -- with its propagated grid when the caller set no node budget (handover), else
+// its input -- solve4_kernel searches it, and its answer is scattered back (sudoku_hip.hip,
+// launch_prop32_solve).  On the 17-clue workload of the headline metric
 // every board is decided here (tools/lockstep_model.py: all of 2,048 solved by propagation).
 //
 // Layout.  Bit b of a 32-bit word is board b of the half's group of 32 (board base + 32 * half + b).
@@ -17,9 +18,9 @@
 // candidate words per cell (c[k][d], bit b set: digit d + 1 is still possible in that cell of board
 // b) and unit hl (rows 0-8, columns 9-17, boxes 18-26).  A triad's cells share their row and box, so
 // the cell update reads five unit records, not seven, and the locked-candidates pass has the
-// presence and eliminations of the lane's own row triad in registers.  A cell is closed when exactly one candidate is
-// left (its single word s[k]); no separate closed state.  Lanes 27..31 run the same code on spare
-// slots (their results are masked out).
+// presence and eliminations of the lane's own row triad in registers.  A cell is closed when exactly
+// one candidate is left (its single word s[k]); no separate closed state.  Lanes 27..31 run the same
+// code on spare slots (their results are masked out).
 //
 // One step for all 32 boards of a half:
 //   singles:  s = exactly-one over the nine words, empty = no candidate, and the cell records
@@ -57,7 +58,7 @@ constexpr uint32_t kP32Rec = 40;         // bytes per cell record: 9 candidate w
 constexpr uint32_t kP32URec = 72;        // bytes per unit record: (T_d, twos_d), d = 0..8
 constexpr uint32_t kP32TRec = 40;        // bytes per triad record: 9 words + pad
 constexpr uint32_t kP32ColTri = 1280;    // the column triads' records (32 row-triad slots before)
-constexpr uint32_t kP32Region = 3456;    // bytes per half: 86 cell records (81 + the spare lanes')
+constexpr uint32_t kP32Region = 3456;    // bytes per half: 81 cell records + the spare lanes' record 81
 constexpr uint32_t kP32Table = 2 * kP32Region;   // p32_unit's read order, 40 B per lane (p32_order_table)
 constexpr uint32_t kP32Lds = kP32Table + 64 * 40;
 constexpr uint32_t kP32Stage = 2592;     // bytes per half of the group's boards (32 x 81)
@@ -237,20 +238,16 @@ __device__ __forceinline__ void p32_upd2(uint32_t& c, uint32_t H, uint32_t anyh,
     c = v;
 }
 
-// the unit summary of the lane's unit (rows 0-8, columns 9-17, boxes 18-26).
-// "In two or more cells" is accumulated two cells at a time after the first three: a bit is in at
-// least two of (ones, a, b) exactly when it is in their majority (bitop3 0xE8), as in solve4's unit4.
-// cell q of the lane's unit at u0 + (q % 3) ua + (q / 3) ub
+// the record offsets of unit j's cells (rows 0-8, columns 9-17, boxes 18-26): cell q at
+// u0 + (q % 3) ua + (q / 3) ub (p32_order_table; j < 27)
 __device__ __forceinline__ void p32_unit_cells(uint32_t j, uint32_t& u0, uint32_t& ua, uint32_t& ub) {
     if (j < 9) {                           // row j: cells 9j + q
         u0 = kP32Rec * 9 * j; ua = kP32Rec; ub = 3 * kP32Rec;
     } else if (j < 18) {                   // column j - 9: cells 9q + (j - 9)
         u0 = kP32Rec * (j - 9); ua = 9 * kP32Rec; ub = 27 * kP32Rec;
-    } else if (j < 27) {                   // box b: rows 3 (b / 3) + q / 3, columns 3 (b % 3) + q % 3
+    } else {                               // box b: rows 3 (b / 3) + q / 3, columns 3 (b % 3) + q % 3
         const uint32_t b = j - 18;
         u0 = kP32Rec * (27 * (b / 3) + 3 * (b % 3)); ua = kP32Rec; ub = 9 * kP32Rec;
-    } else {                               // spare lane: one unwritten record, nine times
-        u0 = kP32Rec * (54 + j); ua = 0; ub = 0;
     }
 }
 
@@ -283,6 +280,9 @@ __device__ __forceinline__ uint32_t p32_dups(const P32Lane& w, const p32_lds_t* 
     return dup;
 }
 
+// The unit summary: "in two or more cells" is accumulated two cells at a time after the first
+// three -- a bit is in at least two of (ones, a, b) exactly when it is in their majority (bitop3
+// 0xE8), as in solve4's unit4.
 // The unit phase's read order.  Step t of every unit lane reads the cell of its unit where the fixed
 // grid kP32Order holds t: kP32Order is a valid Sudoku solution, so at each step the 27 lanes read the
 // same nine cells (one per row, column and box -- each by three lanes, a broadcast), and it is chosen

@@ -57,7 +57,7 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="C4 headline: passes in flight per rank -- consecutive passes issued on this many engine "
                          "contexts in turn (own HIP stream, dequeue state and output buffer each), so one pass's "
                          "launch drain overlaps the next pass's start, as a serving node keeps batches in flight; "

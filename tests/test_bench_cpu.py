@@ -51,9 +51,9 @@ def test_bench_gpus2_launches_two_ranks(tmp_path):
     r = _run_bench(2, tmp=tmp_path)
     assert r["n_gpus"] == 2 and r["scaling"] == "strong"
     assert r["config"]["puzzles_total"] == 301 and r["config"]["puzzles_per_gpu"] in (150, 151)
-    # the single-context pass and both in-flight contexts' outputs are checked
-    assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 3 * 301}
-    assert r["config"]["passes_in_flight_per_gpu"] == 2 and r["single_stream"]["parity"]["mismatched_boards"] == 0
+    # the single-context pass and every in-flight context's output are checked
+    assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 4 * 301}
+    assert r["config"]["passes_in_flight_per_gpu"] == 3 and r["single_stream"]["parity"]["mismatched_boards"] == 0
     assert r["checker"]["parity"] == {"mismatched_boards": 0, "checked_boards": 4000}
     assert list(r)[-2:] == ["checker", "checker_summary"]        # the tail the driver keeps
     assert r["weak_scaling"]["parity"]["mismatched_boards"] == 0
@@ -63,7 +63,7 @@ def test_bench_gpus2_launches_two_ranks(tmp_path):
 def test_bench_gpus1_single_process(tmp_path):
     r = _run_bench(1, tmp=tmp_path)
     assert r["n_gpus"] == 1 and "weak_scaling" not in r
-    assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 3 * 301}
+    assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 4 * 301}
 
 
 def test_bench_gpus2_count_legs_over_tcp_rccl_stub(tmp_path):

@@ -722,7 +722,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         // body ends in an update of the cell words and they keep one register home (with exits in the
         // middle of the step the register allocator gave the words a second home and copied all 27
         // out and back on every step)
-        while (live != 0ull) {
+        // one step (see above); the loop runs two per iteration, so the two copies' register homes of
+        // the cell words can alternate instead of being copied back at every latch
+        auto step = [&]() {
             uint32_t empty, alls;
             p32_singles(w, x, empty, alls);
             __builtin_amdgcn_wave_barrier();
@@ -738,7 +740,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
                 fixw = 0ull;
                 lc = false;
                 __builtin_amdgcn_wave_barrier();
-                continue;
+                return;
             }
             if (it == 0) {   // a digit given twice: not exact, to the search
                 const uint32_t dup = p32_dups(w, lds);
@@ -779,6 +781,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
                 (void)p32_cells<false>(w, x);
             }
             __builtin_amdgcn_wave_barrier();
+        };
+        while (live != 0ull) {
+            step();
+            if (live == 0ull) break;
+            step();
         }
 #if SDK_PROP32_STATS
         if (threadIdx.x == 0) {

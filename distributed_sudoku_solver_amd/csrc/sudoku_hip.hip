@@ -60,9 +60,46 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr size_t kMaxTimedLaunches = 1u << 16;
 
+// A device allocation owned by its holder: freed when the holder goes (sdk_destroy deletes the
+// context after selecting its device), so no buffer added to sdk_ctx can leak.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) {
+        o.p = nullptr;
+        o.bytes = 0;
+    }
+    DevBuf& operator=(DevBuf&& o) noexcept {      // (std::swap of two buffers moves through this)
+        if (this != &o) {
+            if (p) (void)hipFree(p);
+            p = o.p;
+            bytes = o.bytes;
+            o.p = nullptr;
+            o.bytes = 0;
+        }
+        return *this;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(bytes, o.bytes);
+    }
+};
+
+// A host-pointer call that staged through the pinned area: an error return may leave copies
+// from / into it queued, so drain the stream first -- the next call's memcpy into the area (or a
+// grow that frees it) cannot race them.  Disarmed once the call has synchronized.
+struct DrainOnError {
+    hipStream_t s;
+    bool armed;
+    ~DrainOnError() {
+        if (armed) (void)hipStreamSynchronize(s);
+    }
 };
 
 }  // namespace
@@ -738,9 +775,11 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     // the bit-sliced root propagation pass first (prop32_kernel.h): plain solves of whole batches
     // (no first-cell masks, work counters, strided inputs or first-solution scans), 16-byte
     // aligned, at least prop32_min boards; a budget of 1 node is left to solve4 (a board solved at
-    // its root takes one)
+    // its root takes one); prop32 always runs locked-candidates passes, so with SDK_OPT_LOCKED 0
+    // it only runs where no budget can tell the difference
     if (!n_dev && c->prop32 && c->solver == SDK_SOLVER_QUAD && !count_mode && d_out && d_status && !d_work &&
-        !d_mask && in_first == 0 && in_step <= 1 && !c->first_found && (node_budget == 0 || node_budget >= 2) &&
+        !d_mask && in_first == 0 && in_step <= 1 && !c->first_found &&
+        (node_budget == 0 || (node_budget >= 2 && c->locked)) &&
         (int64_t)n >= c->prop32_min && n <= kDnCapBoards &&
         ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15u) == 0)
         return launch_prop32_solve(c, d_in, d_out, d_status, n, order, budget, donate);
@@ -754,7 +793,10 @@ int launch_solve(sdk_ctx* c, const uint8_t* d_in, const uint16_t* d_mask, uint8_
     const bool split_auto = dn == 1;
     const uint64_t split = split_auto ? (!n_dev && n > sdk::kBudgetBigBoards ? 2 * kDnSplitDefault : kDnSplitDefault)
                                       : (uint64_t)dn;
-    c->split_big = split_auto && n_dev ? 2 * kDnSplitDefault : 0;
+    // (only where the node budget leaves room for it: with a budget B <= 256 a board needing
+    // more than B nodes must end as a budget hit, which the split phase at 256 would solve)
+    c->split_big = split_auto && n_dev && (node_budget == 0 || node_budget > 2 * kDnSplitDefault)
+                       ? 2 * kDnSplitDefault : 0;
     const bool two_phase = n > 0 && !count_mode && dn && c->solver == SDK_SOLVER_QUAD &&
                            (eff_order == SDK_ORDER_LEX || eff_order == SDK_ORDER_MRV_UNIQUE) && d_out && d_status &&
                            (node_budget == 0 || node_budget > split) &&
@@ -1020,8 +1062,7 @@ int refine_head(sdk_ctx* c, uint64_t lo, uint64_t mid, uint64_t hi, uint64_t tar
         if ((rc = ensure(nb, (h + tail) * 81))) return rc;
         if (h) HIPCALL(hipMemcpyAsync(nb.p, c->fr_a.p, h * 81, hipMemcpyDeviceToDevice, c->stream));
         HIPCALL(hipStreamSynchronize(c->stream));
-        HIPCALL(hipFree(c->fr_a.p));
-        c->fr_a = nb;
+        c->fr_a.swap(nb);          // the old buffer goes with nb
     }
     HIPCALL(hipMemcpyAsync(static_cast<char*>(c->fr_a.p) + h * 81, c->fr_tail.p, tail * 81, hipMemcpyDeviceToDevice,
                            c->stream));
@@ -1050,6 +1091,7 @@ int expand_boards(sdk_ctx* c, const uint8_t* h_in, const uint16_t* h_masks, uint
         std::memcpy(st, h_in, n * 81);
         if (h_masks) std::memcpy(st + n * 81, h_masks, n * 2);
     }
+    DrainOnError drain{c->stream, true};    // also covers the pageable path's output copy
     HIPCALL(hipMemcpyAsync(c->fr_a.p, st ? st : (const char*)h_in, n * 81, hipMemcpyHostToDevice, c->stream));
     if (h_masks)
         HIPCALL(hipMemcpyAsync(c->fr_mask.p, st ? st + n * 81 : (const char*)h_masks, n * 2, hipMemcpyHostToDevice,
@@ -1065,6 +1107,7 @@ int expand_boards(sdk_ctx* c, const uint8_t* h_in, const uint16_t* h_masks, uint
         if (so) std::memcpy(h_out, so, c->fr_size * 81);
     }
     HIPCALL(hipStreamSynchronize(c->stream));
+    drain.armed = false;
     *out_n = c->fr_size;
     return SDK_OK;
 }
@@ -1196,12 +1239,7 @@ int sdk_destroy(sdk_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    for (DevBuf* b : {&c->dn, &c->dn_stat, &c->dn_in, &c->dn_mask, &c->dn_out, &c->dn_st, &c->dn_work, &c->dn_list,
-                      &c->dn3_in, &c->dn3_mask, &c->dn3_out, &c->dn3_st, &c->dn3_work, &c->dn3_list,
-                      &c->stack, &c->counter, &c->heads, &c->in, &c->mask, &c->out, &c->status, &c->work, &c->verdict,
-                      &c->fr_a, &c->fr_b, &c->prop, &c->bcell, &c->bmask, &c->nchild, &c->offs, &c->fr_status,
-                      &c->fr_mask, &c->tsum, &c->fr_ctl})
-        if (b->p) (void)hipFree(b->p);
+    // every DevBuf member frees itself in `delete c` below (on this device)
     if (c->stage.p) (void)hipHostFree(c->stage.p);
     for (auto& pr : c->events) {
         (void)hipEventDestroy(pr.first);
@@ -1620,6 +1658,7 @@ int sdk_solve_batch_ex(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell
         std::memcpy(s_io, in, n * 81);
         if (first_cell_mask) std::memcpy(s_mask, first_cell_mask, n * 2);
     }
+    DrainOnError drain{c->stream, st != nullptr};
     HIPCALL(hipMemcpyAsync(c->in.p, st ? s_io : in, n * 81, hipMemcpyHostToDevice, c->stream));
     if (first_cell_mask)
         HIPCALL(hipMemcpyAsync(c->mask.p, st ? s_mask : first_cell_mask, n * 2, hipMemcpyHostToDevice, c->stream));
@@ -1632,6 +1671,7 @@ int sdk_solve_batch_ex(sdk_ctx* c, const uint8_t* in, const uint16_t* first_cell
     HIPCALL(hipMemcpyAsync(st ? s_st : status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
     if (work) HIPCALL(hipMemcpyAsync(st ? s_work : work, c->work.p, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCALL(hipStreamSynchronize(c->stream));
+    drain.armed = false;
     if (st) {
         std::memcpy(out, s_io, n * 81);
         std::memcpy(status, s_st, n);

@@ -494,6 +494,26 @@ def _key_trim(hi, key_lo, key_step, g):
     return min(hi, max(0, (g - key_lo) // key_step + 1))
 
 
+def _renormalize_keys(S, g):
+    """Monotone re-keying of the gathered state S (rows lo, hi, local, key_lo, key_step, best,
+    heavy; trimmed at g) in place, computed identically on every rank.  The ranks' live ranges
+    occupy disjoint key intervals, so ordered by the key of their first board they are laid end
+    to end with one common step; the lowest hit g maps above every live key and the other hits
+    (all above g, so never the answer) are dropped.  The step leaves room for key_lo = base -
+    lo * step to stay within int64 (lo is an index into a frontier of at most 2^25 boards)."""
+    live = sorted((k for k in range(len(S)) if S[k][1] > S[k][0]), key=lambda k: S[k][3] + S[k][0] * S[k][4])
+    total = sum(S[k][1] - S[k][0] for k in live)
+    step = max(1, KEY_SPACE // (total + max((S[k][0] for k in live), default=0) + 1))
+    base = 0
+    for k in live:
+        S[k][3], S[k][4] = base - S[k][0] * step, step
+        base += (S[k][1] - S[k][0]) * step
+    for s in S:
+        if s[1] <= s[0]:
+            s[3], s[4] = 0, step
+        s[5] = KEY_SPACE + 1 if (g != INT64_MAX and s[5] == g) else INT64_MAX
+
+
 def sharded_solve(engine, board, rank, world, comm=None, mask=None, target=None, chunk=None, info=None,
                   ranges=None, round_budget=None):
     """First completion of `board` in the reference's DFS order, split over `world` ranks.
@@ -519,7 +539,9 @@ def sharded_solve(engine, board, rank, world, comm=None, mask=None, target=None,
         others;
       * before every round the ranks all-gather (lo, hi, local, key_lo, key_step, best_key, heavy)
         (RCCL ncclAllGather of 7 x int64 per rank): the minimum best_key is the found flag --
-        every rank drops its boards keyed above it -- and rebalance_plan gives dry ranks the
+        every rank drops its boards keyed above it, and all ranks re-key the live boards over the
+        whole key space with one monotone map (_renormalize_keys: refinements never exhaust the
+        keys) -- and rebalance_plan gives dry ranks the
         upper half of the largest live range, as board RECORDS (grouped ncclSend/ncclRecv) when
         either side no longer holds the replicated frontier.  A rank whose remainder is one board
         (or heavy: it hit the budget) refines it while another is dry, so one heavy subtree does
@@ -571,6 +593,11 @@ def sharded_solve(engine, board, rank, world, comm=None, mask=None, target=None,
                     s[6] = 0
             if all(s[1] <= s[0] for s in S):
                 break
+            # re-spread the live keys over the whole key space (same map on every rank): repeated
+            # refinements only divide a rank's own interval, so without this a long search runs
+            # out of integer keys
+            _renormalize_keys(S, g)
+            key_lo, key_step, my_best = S[rank if comm is not None else 0][3:6]
             skip = False
             if comm is not None:
                 newS, moves, refines = rebalance_plan([s[:3] + [s[6]] for s in S], min_split=split)

@@ -170,3 +170,43 @@ def test_prop32_options_validated(engine):
         with pytest.raises(Exception):
             engine.set_option(key, bad)
     assert engine.get_option(L.SDK_OPT_PROP32) == 1
+
+
+def test_prop32_fallback_split_phase_within_node_budget(engine):
+    """a prop32 fallback batch with more than 2^19 undecided boards splits at 256 nodes
+    only where the caller's node budget is above that; with a budget B <= 256 the split phase stays
+    at 128, so no board is finished there past B nodes.  The split phase is one slot per board
+    (deterministic), so the count of boards it passes on is the witness: the same under B = 129 and
+    200 (split 128), more than under B = 0 or 300 (split 256).  Decided boards equal their known
+    solutions; budget hits come back as their input."""
+    engine.set_option(L.SDK_OPT_PROP32, 1)
+    boards, sol = synth.make_hard_sym(1 << 20, threads=8)
+    passed = {}
+    for b in (0, 300, 129, 200):
+        out, st, _ = engine.solve_batch(boards, budget=b)
+        assert engine.get_option(L.SDK_OPT_PROP32_UNDECIDED) > (1 << 19)
+        assert set(np.unique(st).tolist()) <= {1, L.SDK_BUDGET_HIT}, b
+        assert np.array_equal(out[st == 1], sol[st == 1]), b
+        assert np.array_equal(out[st != 1], boards[st != 1]), b
+        if b == 0:
+            assert (st == 1).all()
+        passed[b] = engine.get_option(L.SDK_OPT_SPLIT_BOARDS)
+    assert passed[129] == passed[200] > passed[0] == passed[300], passed
+
+
+def test_prop32_not_used_without_locked_candidates_under_budget(engine):
+    """prop32 always runs locked-candidates passes, so with SDK_OPT_LOCKED 0 and a node
+    budget the search alone runs (one span); without a budget the pass still runs (two spans)."""
+    engine.set_option(L.SDK_OPT_PROP32, 1)
+    engine.set_option(L.SDK_OPT_LOCKED, 0)
+    try:
+        boards, sol = synth.make_17clue(8192, seed=4)
+        for budget, spans_want in ((1000, 1), (0, 2)):
+            engine.timer_reset()
+            out, st, _ = engine.solve_batch(boards, budget=budget)
+            _, spans = engine.timer_read()
+            engine.timer_stop()
+            assert spans == spans_want, budget
+            assert np.array_equal(out[st == 1], sol[st == 1])
+    finally:
+        engine.set_option(L.SDK_OPT_LOCKED, 1)

@@ -71,3 +71,46 @@ def test_synth_30clue_and_check_boards():
     b, exp = synth.make_check_boards(20000, seed=11)
     assert (O.check_batch(b, 4) == exp).all()
     assert 0.45 < (exp == 3).mean() < 0.55
+
+
+def test_renormalize_keys_monotone_and_in_range():
+    """shard._renormalize_keys: the live boards of all ranks keep their lex order,
+    land in [0, KEY_SPACE), key_lo stays in int64, the lowest hit maps above every live key."""
+    from distributed_sudoku_solver_amd.shard import KEY_SPACE, INT64_MAX, _renormalize_keys
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        w = int(rng.integers(1, 9))
+        S, base = [], 0
+        for k in rng.permutation(w):            # disjoint key intervals in a random rank order
+            lo = int(rng.integers(0, 1 << 25))
+            n = int(rng.integers(0, 40))
+            step = int(rng.integers(1, 1 << 20))
+            S.append([k, lo, lo + n, 0, base - lo * step, step, INT64_MAX, 0])
+            base += n * step + int(rng.integers(0, 1 << 30))
+        S = [s[1:] for s in sorted(S)]
+        g = INT64_MAX if rng.integers(0, 2) else base
+        if g != INT64_MAX:
+            S[0][5] = g
+        before = sorted((s[3] + t * s[4], r, t) for r, s in enumerate(S) for t in range(s[0], s[1]))
+        _renormalize_keys(S, g)
+        after = sorted((s[3] + t * s[4], r, t) for r, s in enumerate(S) for t in range(s[0], s[1]))
+        assert [x[1:] for x in before] == [x[1:] for x in after]
+        assert all(0 <= x[0] < KEY_SPACE for x in after)
+        assert all(-(1 << 63) <= s[3] < (1 << 63) and s[4] >= 1 for s in S)
+        assert [s[5] for s in S] == [KEY_SPACE + 1 if (g != INT64_MAX and r == 0) else INT64_MAX
+                                     for r in range(len(S))]
+
+
+def test_sharded_solve_thousands_of_refinements():
+    """a long first-solution search (S1 under a 1-node round budget, one board per
+    refinement head: ~3,200 refinements) no longer runs out of lex keys; answer = the seed's."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from doubles import OracleEngine
+    from distributed_sudoku_solver_amd.shard import sharded_solve
+    info = {}
+    out, st = sharded_solve(OracleEngine(), synth.parse(synth.SEEDS17["S1"]), 0, 1, target=1, round_budget=1,
+                            info=info)
+    assert st == 1 and "".join(map(str, out)) == synth.SEED_SOLUTIONS["S1"]
+    assert info["refines"] > 1000, info

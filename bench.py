@@ -102,6 +102,8 @@ def parse_args():
     ap.add_argument("--c5-boards", default="15,14",
                     help="C5 boards: 16/15/14 clues (S1 with clues removed; counts 7,309 / 3,481,026 / 18,204,270); "
                          "the first is counted by the two-stage split, the second by the rebalanced one")
+    ap.add_argument("--first-boards", default="heaviest,S1,S2",
+                    help="first-solution leg (sharded_solve over all ranks): boards, heaviest or S1..S5 ('' = skip)")
     ap.add_argument("--frontier-probe", type=int, default=1_000_000,
                     help="boards of the timed one-board frontier build beside the rebalanced count (0 = skip)")
     ap.add_argument("--lane-puzzles", type=int, default=200_000,
@@ -245,6 +247,7 @@ def cpu_baseline_c(puzzles, seconds, threads):
         "unit": "puzzles/s",
         "cores": threads,
         "kind": "port",
+        "attempted": done, "solved": solved, "capped": timeouts,
         "sample": (f"first {done} puzzles of the rank-0 batch, naive DFS in C (oracle/sudoku_oracle.c, "
                    f"restates DHT_Node.py:474-538, validations-exact), {threads} threads, "
                    f"{wall:.1f} s wall, {timeouts} hit the 2e9-validation budget"),
@@ -275,6 +278,11 @@ def cpu_baseline_python(puzzles, seconds, procs, budget, what):
         "unit": "puzzles/s",
         "cores": procs,
         "kind": "port",
+        "attempted": done, "solved": solved, "capped": timeouts,
+        # puzzles stopped at the per-puzzle cap are not counted and their time is: with capped > 0 the
+        # sample's solved puzzles are its easiest, and the rate an upper bound of the CPU's rate on them
+        "value_is": ("an upper bound: solved puzzles per second of a sample whose capped puzzles were dropped "
+                     "(the easiest slice)" if timeouts else "solved puzzles per second, every puzzle solved"),
         "sample": (f"{what}: {done} puzzles attempted in {procs} disjoint slices, one process per core, "
                    f"pure-Python naive DFS (oracle/oracle.py py_naive_solve, restates DHT_Node.py:474-538 "
                    f"line by line, -d 0), {solved} solved, {timeouts} stopped at the {budget:,}-validation "
@@ -444,6 +452,54 @@ def c5_rebalanced_leg(eng, d, args, synth):
             "ok": total == expected and st == 1, "frontier_boards": size,
             "rounds": info.get("rounds"), "steals": info.get("steals"),
             "wall_ms": w * 1000.0, "value": total / w, "unit": "solutions/s"}
+
+
+def first_board(synth, name):
+    """A first-solution board of the sharded_solve leg -> (board, its lex-first completion, what).
+    `heaviest`: the committed hard set's heaviest puzzle (most singles-DFS nodes, unique);
+    `S1`..`S5`: the survey's 17-clue seeds (0.67M-83M reference validations each)."""
+    if name == "heaviest":
+        hp, hs = synth.make_hard_heaviest(1, threads=cpu_share())
+        return hp[0], hs[0], "the committed hard set's heaviest puzzle"
+    return (synth.parse(synth.SEEDS17[name]), synth.parse(synth.SEED_SOLUTIONS[name]),
+            f"17-clue seed {name} (SURVEY App. A)")
+
+
+def first_solution_leg(eng, d, args, synth):
+    """North star's single hard search split over the GPUs (the reference splits one
+    search between ring nodes, DHT_Node.py:491-510): shard.sharded_solve on each board -- every
+    rank builds the same lex-ordered frontier, searches its block in rounds, all-gathers (lo, hi,
+    keys, best) over RCCL (xGMI) as the found flag and rebalances by moving frontier records
+    (grouped ncclSend/ncclRecv) -- answer checked against the board's known completion."""
+    from distributed_sudoku_solver_amd.shard import RcclComm, sharded_solve
+    comm = RcclComm(eng, d.rank, d.world, transport=d.comm) if d.world > 1 else None
+    res, ok = {}, True
+    try:
+        for name in args.first_boards.split(","):
+            board, sol, what = first_board(synth, name)
+            sharded_solve(eng, board, d.rank, d.world, comm=comm)      # warm-up
+            best = None
+            for _ in range(3):
+                info = {}
+                d.barrier()
+                t0 = time.perf_counter()
+                out, st = sharded_solve(eng, board, d.rank, d.world, comm=comm, info=info)
+                w = d.max(time.perf_counter() - t0)
+                good = st == 1 and bool(np.array_equal(np.asarray(out, np.uint8), sol))
+                ok &= good
+                if best is None or w < best[0]:
+                    best = (w, info, good)
+            w, info, good = best
+            res[name] = {"board": what, "wall_ms": 1000.0 * w, "ok": good, "rounds": info.get("rounds"),
+                         "moved_records": info.get("moved_records"), "refines": info.get("refines"),
+                         "steals": info.get("steals"), "frontier_boards": info.get("frontier")}
+    finally:
+        if comm is not None:
+            comm.close()
+    res["workload"] = (f"first (lex-first) completion of one board, its lex frontier split over {d.world} GPU(s)"
+                       + (": RCCL all-gather found flag + record moves" if d.world > 1 else ""))
+    res["ok"] = ok
+    return res
 
 
 def minimal_leg(eng, d, args, synth, L):
@@ -688,6 +744,17 @@ def http_leg(requests, api="dht"):
 def _checker_last(result, leg):
     """The C3 checker leg goes at the END of the line (the driver keeps only
     the tail of stdout), with its headline figures first in a compact summary."""
+    # the headline kernel's rooflines first, compact (VERDICT r5 item 1: visible in the driver's tail)
+    rf = result.get("roofline") or {}
+    v = rf.get("valu") or {}
+    if rf:
+        result.pop("roofline_summary", None)
+        result["roofline_summary"] = {
+            "kernel": rf.get("kernel"), "avg_kernel_ms": rf.get("avg_kernel_ms"), "hbm_frac": rf.get("frac"),
+            "valu_frac": v.get("frac"), "valu_per_quad": v.get("valu_per_quad"),
+            "mix_ceiling_frac": (v.get("mix_ceiling") or {}).get("frac"), "clock_ghz": v.get("clock_ghz"),
+            "clock_measured_live": bool(v.get("clock")),
+            "valu_frac_at_2p4ghz": (v.get("at_2p4ghz_cap") or {}).get("frac")}
     if leg is None:
         return
     result.pop("checker", None)
@@ -740,7 +807,35 @@ def timer_spans(e):
     return list(arr[:min(cnt.value, cap)])
 
 
-def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=True):
+def kernel_clock(e, d_in, d_out, d_st, n, launches=20):
+    """In-kernel shader clock of the prop32 pass, measured live: `launches` more back-to-back passes
+    over the same resident boards with the diagnostic twin of the kernel (prop32_clock_kernel:
+    s_memtime / s_memrealtime stamped at each workgroup's entry and exit, nothing else changed;
+    MI355X_MICROARCH.md "DVFS give-back" item 6); the last pass's workgroups give the median
+    clock.  None for an engine without the diagnostic (the CPU tests' stub)."""
+    from distributed_sudoku_solver_amd import _lib as L
+    lib = getattr(e, "lib", None)
+    if lib is None or not hasattr(lib, "sdk_debug_clock_arm"):
+        return None
+    L.check(lib.sdk_debug_clock_arm(e.ctx, 1), "sdk_debug_clock_arm")
+    try:
+        for _ in range(launches):
+            e.solve_batch_dev(d_in, d_out, d_st, n)
+        e.synchronize()
+        out4 = (ctypes.c_double * 4)()
+        wgs = ctypes.c_int64()
+        L.check(lib.sdk_debug_clock_read(e.ctx, out4, ctypes.byref(wgs)), "sdk_debug_clock_read")
+    finally:
+        lib.sdk_debug_clock_arm(e.ctx, 0)
+    if wgs.value == 0:
+        return None
+    return {"ghz": out4[0], "ghz_p10": out4[1], "ghz_p90": out4[2], "ghz_mean": out4[3], "workgroups": wgs.value,
+            "launches": launches,
+            "source": "s_memtime / s_memrealtime per workgroup of the last of these back-to-back passes "
+                      "(prop32_clock_kernel, the stamped twin of the timed kernel), median"}
+
+
+def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=True, clock=False):
     """Time `steps` sdk_solve_batch_dev passes over this rank's resident slice (barrier +
     device sync on both sides, max over ranks); verify every board afterwards.  Each rank's clock
     runs from the release of the opening barrier to its own device sync at the end, and the job's
@@ -751,9 +846,10 @@ def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=
     (engine.fork(): each its own HIP stream, dequeue state, DFS stacks and output buffer), so that
     one pass's launch drain -- the last chunks finishing while most of the GPU idles, ~0.3 ms at
     every batch size -- overlaps the next pass's start: batches in flight, as a serving node keeps
-    them.  Every pass solves the whole slice; every output buffer is checked.  (The headline uses
-    one context: its per-launch HIP events are then the kernel's own duration, the roofline's
-    denominator; overlapped launches' events also hold their wait for the GPU.)"""
+    them.  Every pass solves the whole slice; every output buffer is checked.  (The headline's
+    `value` uses three contexts; its `single_stream` figure, one context, supplies the per-launch
+    HIP events -- the kernel's own duration, the roofline's denominator: overlapped launches'
+    events would also hold their wait for the GPU.)"""
     from distributed_sudoku_solver_amd import _lib as L
     n = len(puzzles)
     nctx = max(1, min(int(contexts), max(1, steps)))
@@ -792,6 +888,8 @@ def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=
                 spans = spans[0::2]
             kernel_ms += sum(spans)
             launches += len(spans)
+    # the clock the timed passes ran at: more passes of the same kind straight after them (events off)
+    solve_leg.clock = kernel_clock(eng, d_in, outs[0][0], outs[0][1], n) if clock else None
     elapsed_max = d.max(elapsed)
     bad = 0
     out = np.empty((n, 81), np.uint8)
@@ -910,10 +1008,11 @@ def main():
     # one context first: its per-launch HIP events are the kernel's own duration (the roofline's
     # denominator); then the headline with `inflight` passes in flight (every pass solves the whole
     # slice, every output buffer is checked)
-    s_el, avg_kernel_s, bad_total = solve_leg(eng, d, args, puzzles, expected, args.steps, args.warmup)
+    s_el, avg_kernel_s, bad_total = solve_leg(eng, d, args, puzzles, expected, args.steps, args.warmup,
+                                              clock=args.solver == "quad" and "prop32" in solve_kernel)
     single_stream = {"value": total * args.steps / s_el, "unit": "puzzles/s", "ms_per_step": s_el / args.steps * 1e3,
                      "avg_kernel_ms": avg_kernel_s * 1e3, "contexts": 1,
-                     "avg_fallback_ms": solve_leg.fallback_ms,
+                     "avg_fallback_ms": solve_leg.fallback_ms, "clock": solve_leg.clock,
                      "parity": {"mismatched_boards": bad_total, "checked_boards": total}}
     inflight = max(1, args.inflight)
     if inflight > 1:
@@ -945,14 +1044,16 @@ def main():
                 "algorithmic B per puzzle)",
     }
     prec = pipe_record(args.pmc_pipe, "c4", n) if args.workload == "solve17" else None
-    if prec and prec.get("valu_insts") and prec.get("clock_ghz"):
-        # per SIMD, from a PMC pass of this exact launch (tools/pmc_r04.sh, tools/pmc_pipe_summary.py),
-        # priced at the issue peak of 2 wave64 VALU per SIMD quad-cycle at the profiled clock; beside
-        # it the ceiling this kernel's own instruction mix reaches on this GPU (tools/issue_calib.hip:
-        # its 3-source VOP3 and packed VOP3P ops do not dual-issue, so the mix tops out near one per
-        # quad-cycle with every SIMD full)
-        quads_per_s = 256 * 4 * prec["clock_ghz"] * 1e9 / 4
-        peak = quads_per_s * VALU_PER_SIMD_QUAD
+    clk = single_stream.get("clock")
+    if prec and prec.get("valu_insts"):
+        # VALU wave-instructions per launch from a PMC pass of this exact launch (tools/pmc_r04.sh,
+        # tools/pmc_pipe_summary.py; an instruction count does not depend on the clock) over the
+        # timed kernel's duration, priced at the issue peak of 2 wave64 VALU per SIMD quad-cycle AT
+        # THE CLOCK THE TIMED PASSES RAN AT (measured live in this run, kernel_clock; the profiled
+        # run's clock is lower and would overstate every fraction), and beside it
+        # at the 2.4 GHz cap.  Next to the peak: the ceiling this kernel's own instruction mix reaches
+        # on this GPU (tools/issue_calib.hip: 3-source VOP3 and packed VOP3P ops do not dual-issue,
+        # so the mix tops out near one per quad-cycle with every SIMD full)
         rate = prec["valu_insts"] / avg_kernel_s
         mix = mix_ceiling(args.issue_calib)
         # the kernel's own mix: prop32's step is 3-source VOP3 (v_bitop3 / v_or3) almost throughout --
@@ -960,14 +1061,26 @@ def main():
         p32 = "prop32" in solve_kernel
         mix_key = "k_or3@8" if p32 else "k_mix@8"
         mix_q = (mix or {}).get(mix_key, {}).get("valu_per_quad")
+
+        def priced(ghz):
+            quads_per_s = 256 * 4 * ghz * 1e9 / 4
+            peak = quads_per_s * VALU_PER_SIMD_QUAD
+            return {"clock_ghz": ghz, "peak": peak, "frac": rate / peak, "valu_per_quad": rate / quads_per_s,
+                    "mix_ceiling_frac": rate / (mix_q * quads_per_s) if mix_q else None}
+        at = priced(clk["ghz"]) if clk else priced(2.4)
+        cap = priced(2.4)
         roofline["valu"] = {
-            "bound": "valu-issue", "achieved": rate, "unit": "wave-instr/s", "peak": peak,
+            "bound": "valu-issue", "achieved": rate, "unit": "wave-instr/s", "peak": at["peak"],
+            "clock_ghz": at["clock_ghz"],
+            "clock_source": (clk["source"] if clk else "no live clock: the 2.4 GHz cap (fractions are then lower bounds)"),
+            "clock": clk,
             "peak_note": "2 wave64 VALU per SIMD quad-cycle (one per 2 cycles on a SIMD-32, MI355X_MICROARCH.md:54) "
-                         "x 1024 SIMDs at the profiled clock",
-            "frac": rate / peak,
-            "valu_per_quad": rate / quads_per_s,
-            "mix_ceiling": ({"valu_per_quad": mix_q, "wave_instr_per_s": mix_q * quads_per_s,
-                             "frac": rate / (mix_q * quads_per_s), "calibration_kernel": mix_key,
+                         "x 1024 SIMDs at clock_ghz",
+            "frac": at["frac"],
+            "valu_per_quad": at["valu_per_quad"],
+            "at_2p4ghz_cap": cap,
+            "mix_ceiling": ({"valu_per_quad": mix_q, "wave_instr_per_s": mix_q * 256 * at["clock_ghz"] * 1e9,
+                             "frac": at["mix_ceiling_frac"], "calibration_kernel": mix_key,
                              "note": ("tools/issue_calib.hip k_or3 (independent v_or3_b32 chains, ~4.4 waves per "
                                       "SIMD): prop32's step is v_bitop3 / v_or3 throughout; 3-source VOP3 ops "
                                       "dual-issue in ~7 % of quad-cycles (2-operand VOP2 ops: 78 %)" if p32 else
@@ -976,9 +1089,10 @@ def main():
                                       "dual-issue in ~7 % of quad-cycles (2-operand VOP2 ops: 78 %)"),
                              "calibration": mix, "source": os.path.relpath(args.issue_calib, ROOT)}
                             if mix_q else None),
+            "profiled_clock_ghz": prec.get("clock_ghz"),
             "issue_busy_frac": prec["valu_busy_frac"],
-            "issue_busy_note": "SIMD quad-cycles with any VALU issue: (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / "
-                               "quad-cycles; dual issue in valu_dual_frac of them",
+            "issue_busy_note": "SIMD quad-cycles with any VALU issue in the profiled run: (SQ_INSTS_VALU - "
+                               "SQ_ACTIVE_INST_VALU2) / quad-cycles; dual issue in valu_dual_frac of them",
             "valu_insts_per_puzzle": prec["valu_insts"] / n,
             "lds_insts_per_puzzle": (prec.get("lds_insts") or 0) / n,
             "salu_insts_per_puzzle": (prec.get("salu_insts") or 0) / n,
@@ -1085,6 +1199,13 @@ def main():
         side("c5_count", lambda: c5_leg(eng, d, args, synth))
         side("c5_count_rebalanced", lambda: c5_rebalanced_leg(eng, d, args, synth))
 
+    # ------------------------------------- one hard search split over the GPUs
+    if args.first_boards and getattr(args, "shared_gpus", False):
+        result["first_solution"] = {"skipped": "more ranks than GPUs: RCCL needs one device per rank"}
+    elif args.first_boards:
+        leg = side("first_solution", lambda: first_solution_leg(eng, d, args, synth))
+        bad_total += 1 if leg.get("ok") is False else 0       # a wrong answer fails the run
+
     # ---------------------------------------------------------- CPU baseline
     if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
         cores = args.cpu_cores or cpu_share()
@@ -1092,7 +1213,12 @@ def main():
         result["cpu_baseline"] = cpu_baseline_python(puzzles[:cores * 64], args.cpu_seconds, cores,
                                                      args.cpu_puzzle_budget, "C4 17-clue sample")
         result["cpu_baseline"]["reference_measured"] = REFERENCE_MEASURED["solve_17clue"]
-        result["cpu_baseline_c_port"] = cpu_baseline_c(puzzles, args.cpu_seconds, cores)
+        # the same DFS in C, uncapped (every attempted puzzle solved), on the same stream
+        result["cpu_baseline"]["c_port"] = cpu_baseline_c(puzzles, args.cpu_seconds, cores)
+        hs = result.get("hard_search", {}).get("cpu_baseline_c_port")
+        if hs:     # the hard set's C-port rate, beside the GPU's hard_search figures
+            result["cpu_baseline"]["hard_set_c_port"] = {k: hs[k] for k in ("value", "unit", "cores", "attempted",
+                                                                             "solved", "capped") if k in hs}
 
     if d.rank == 0 and d.world == 1 and args.http_requests > 0:
         side("post_solve_latency", lambda: http_leg(args.http_requests))

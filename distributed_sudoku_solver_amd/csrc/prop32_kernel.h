@@ -643,10 +643,19 @@ __device__ __forceinline__ void p32_order_table(p32_lds_t* lds) {
 #ifndef SDK_PROP32_WAVES_PER_EU
 #define SDK_PROP32_WAVES_PER_EU 4
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_WAVES_PER_EU))) void prop32_kernel(
-    Prop32Args a) {
+// The kernel body; kStamp (prop32_clock_kernel, a diagnostic twin: the timed kernel runs no stamp)
+// writes s_memtime (shader clock) and s_memrealtime (100 MHz) at a workgroup's entry and exit to
+// stamps[4 blockIdx.x ..], a buffer nothing else reads: the in-kernel clock of a launch is
+// their ratio (MI355X_MICROARCH.md, "DVFS give-back" item 6), the clock the VALU roofline prices
+template <bool kStamp>
+__device__ __forceinline__ void prop32_body(Prop32Args a, uint64_t* stamps) {
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[kP32Lds];
     p32_lds_t* const lds = (p32_lds_t*)s_lds;
+    if (kStamp && threadIdx.x == 0) {    // (stored at once: no register holds them through the loop)
+        uint64_t* o = stamps + 4u * blockIdx.x;
+        o[0] = __builtin_amdgcn_s_memtime();
+        o[1] = __builtin_amdgcn_s_memrealtime();
+    }
     p32_order_table(lds);
     __builtin_amdgcn_wave_barrier();
     P32Lane w;
@@ -870,6 +879,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_W
         }
         __builtin_amdgcn_wave_barrier();
     }
+    if (kStamp) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            uint64_t* o = stamps + 4u * blockIdx.x;
+            o[2] = t1;
+            o[3] = r1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_WAVES_PER_EU))) void prop32_kernel(
+    Prop32Args a) {
+    prop32_body<false>(a, nullptr);
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDK_PROP32_WAVES_PER_EU))) void prop32_clock_kernel(
+    Prop32Args a, uint64_t* stamps) {
+    prop32_body<true>(a, stamps);
 }
 #endif
 

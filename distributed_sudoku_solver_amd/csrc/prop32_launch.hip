@@ -6,8 +6,12 @@
 
 namespace sdk {
 
-hipError_t launch_prop32(const Prop32Args& a, unsigned grid, hipStream_t stream) {
-    prop32_kernel<<<grid, 64, 0, stream>>>(a);
+// stamps non-null: the diagnostic twin that records the in-kernel clock (prop32_body)
+hipError_t launch_prop32(const Prop32Args& a, unsigned grid, hipStream_t stream, uint64_t* stamps) {
+    if (stamps)
+        prop32_clock_kernel<<<grid, 64, 0, stream>>>(a, stamps);
+    else
+        prop32_kernel<<<grid, 64, 0, stream>>>(a);
     return hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ namespace sdk {
 hipError_t launch_solve2(const SolveArgs& a, unsigned grid, hipStream_t stream);
 hipError_t launch_solve4(const SolveArgs& a, unsigned grid, hipStream_t stream);
 int solve4_dn_blocks_per_cu();   // resident workgroups per CU of solve4_kernel<true>
-hipError_t launch_prop32(const Prop32Args& a, unsigned grid, hipStream_t stream);
+hipError_t launch_prop32(const Prop32Args& a, unsigned grid, hipStream_t stream, uint64_t* stamps);
 hipError_t launch_p32_scatter(const uint32_t* list, const uint8_t* sub_out, const int8_t* sub_st, const uint8_t* in,
                               uint8_t* out, int8_t* status, unsigned grid, hipStream_t stream);
 hipError_t launch_expand4(const ExpandArgs& a, unsigned grid, hipStream_t stream);   // expand4_kernel.h
@@ -366,6 +366,9 @@ struct sdk_ctx {
     int prop32_tail_step = 24;     //     from this step on (SDK_OPT_PROP32_TAIL = live | step << 8)
     bool prop32_ran = false;       // the last solve ran it (p32_list[0] = its undecided boards)
     DevBuf p32_ctl, p32_list, p32_in, p32_out, p32_st;
+    int clock_probe = 0;           // sdk_debug_clock_arm: prop32 passes run the stamped twin
+    DevBuf p32_stamps;             // ... its stamps, 4 words per workgroup of the last such pass
+    uint32_t p32_stamp_wgs = 0;
     DevBuf fr_a, fr_b, prop, bcell, bmask, nchild, offs, fr_status, fr_mask, tsum, fr_ctl;
     DevBuf fr_tail;                // refine_head: the boards kept after the refined ones
     // the device-resident frontier of the last sdk_frontier_build (in fr_a)
@@ -877,7 +880,13 @@ int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t*
     a.tail_step = (uint32_t)c->prop32_tail_step;
     const uint64_t groups = (n + 63) / 64;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(groups, (uint64_t)c->cus * 20));
-    HIPCALL(sdk::launch_prop32(a, grid, c->stream));
+    uint64_t* stamps = nullptr;
+    if (c->clock_probe) {      // the diagnostic twin (sdk_debug_clock_arm)
+        if ((rc = ensure(c->p32_stamps, (size_t)grid * 32))) return rc;
+        stamps = static_cast<uint64_t*>(c->p32_stamps.p);
+        c->p32_stamp_wgs = grid;
+    }
+    HIPCALL(sdk::launch_prop32(a, grid, c->stream, stamps));
     if ((rc = timer_end(c, stop)) || (rc = timer_begin(c, &stop))) return rc;
     c->timer_hold = true;
     c->prop32_ran = true;
@@ -1376,6 +1385,46 @@ extern "C" int sdk_debug_dn_ctl(sdk_ctx* c, uint32_t* out16) {
     HIPCALL(hipSetDevice(c->device));
     HIPCALL(hipMemcpyAsync(out16, c->dn.p, 64, hipMemcpyDeviceToHost, c->stream));   // the global words
     HIPCALL(hipStreamSynchronize(c->stream));
+    return SDK_OK;
+}
+
+// diagnostics (not in the header): the in-kernel clock of the prop32 pass.  Armed, the context's
+// prop32 passes run prop32_clock_kernel, which stamps s_memtime / s_memrealtime at each workgroup's
+// entry and exit; _read waits for the last such pass and returns the shader clock of its workgroups
+// (GHz: shader ticks per 10 ns of the 100 MHz real-time counter) as median, 10th and 90th percentile
+// and mean (out4), and how many workgroups it had.  (MI355X_MICROARCH.md, "DVFS give-back" item 6.)
+extern "C" int sdk_debug_clock_arm(sdk_ctx* c, int on) {
+    if (!c) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->clock_probe = on ? 1 : 0;
+    return SDK_OK;
+}
+
+extern "C" int sdk_debug_clock_read(sdk_ctx* c, double* out4, int64_t* workgroups) {
+    if (!c || !out4 || !workgroups) return fail(SDK_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    *workgroups = 0;
+    for (int i = 0; i < 4; ++i) out4[i] = 0.0;
+    if (!c->p32_stamp_wgs || !c->p32_stamps.p) return SDK_OK;
+    HIPCALL(hipSetDevice(c->device));
+    std::vector<uint64_t> h((size_t)c->p32_stamp_wgs * 4);
+    HIPCALL(hipMemcpyAsync(h.data(), c->p32_stamps.p, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCALL(hipStreamSynchronize(c->stream));
+    std::vector<double> ghz;
+    ghz.reserve(c->p32_stamp_wgs);
+    for (size_t w = 0; w < c->p32_stamp_wgs; ++w) {
+        const uint64_t dt = h[4 * w + 2] - h[4 * w], dr = h[4 * w + 3] - h[4 * w + 1];
+        if (dr >= 10 && h[4 * w + 2] > h[4 * w]) ghz.push_back((double)dt / (double)dr / 10.0);   // >= 0.1 us
+    }
+    if (ghz.empty()) return SDK_OK;
+    std::sort(ghz.begin(), ghz.end());
+    double sum = 0.0;
+    for (double v : ghz) sum += v;
+    out4[0] = ghz[ghz.size() / 2];
+    out4[1] = ghz[ghz.size() / 10];
+    out4[2] = ghz[(ghz.size() * 9) / 10];
+    out4[3] = sum / (double)ghz.size();
+    *workgroups = (int64_t)ghz.size();
     return SDK_OK;
 }
 

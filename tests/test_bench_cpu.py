@@ -38,6 +38,7 @@ def _run_bench(gpus, extra=(), tmp=None):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "2", "--warmup", "1",
            "--workload", "solve30", "--batch", "301", "--check-boards", "2000", "--check-steps", "1",
            "--check-warmup", "1", "--c2-puzzles", "0", "--minimal-puzzles", "0", "--hard-leg", "0", "--count-leg", "0", "--lane-puzzles", "0",
+           "--first-boards", "",
            "--cpu-seconds", "0",
            "--http-requests", "0", "--pmc-summary", "", "--engine-factory", "doubles:BenchStubEngine", *extra]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
@@ -55,7 +56,7 @@ def test_bench_gpus2_launches_two_ranks(tmp_path):
     assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 4 * 301}
     assert r["config"]["passes_in_flight_per_gpu"] == 3 and r["single_stream"]["parity"]["mismatched_boards"] == 0
     assert r["checker"]["parity"] == {"mismatched_boards": 0, "checked_boards": 4000}
-    assert list(r)[-2:] == ["checker", "checker_summary"]        # the tail the driver keeps
+    assert list(r)[-3:] == ["roofline_summary", "checker", "checker_summary"]   # the tail the driver keeps
     assert r["weak_scaling"]["parity"]["mismatched_boards"] == 0
     assert r["value"] > 0 and r["steps"] == 2 and r["warmup"] == 1
 
@@ -74,6 +75,17 @@ def test_bench_gpus2_count_legs_over_tcp_rccl_stub(tmp_path):
         assert r[leg].get("ok") is True, r[leg]
         assert r[leg]["solutions"] == 7309
     assert r["c5_count_rebalanced"]["rounds"] >= 1
+
+
+def test_bench_gpus2_first_solution_leg(tmp_path):
+    """the first-solution leg (shard.sharded_solve over the ranks' RCCL stub) at
+    world 2 on a heavy 17-clue seed: the known completion, and its rounds / moves / refinements."""
+    r = _run_bench(2, extra=["--first-boards", "S4"], tmp=tmp_path)
+    leg = r["first_solution"]
+    assert leg["ok"] is True and leg["S4"]["ok"] is True, leg
+    for key in ("wall_ms", "rounds", "moved_records", "refines", "steals", "frontier_boards"):
+        assert leg["S4"][key] is not None, key
+    assert leg["S4"]["rounds"] >= 1
 
 
 def test_no_torch_blocker_works(tmp_path):

@@ -175,10 +175,12 @@ def test_prop32_options_validated(engine):
 def test_prop32_fallback_split_phase_within_node_budget(engine):
     """a prop32 fallback batch with more than 2^19 undecided boards splits at 256 nodes
     only where the caller's node budget is above that; with a budget B <= 256 the split phase stays
-    at 128, so no board is finished there past B nodes.  The split phase is one slot per board
-    (deterministic), so the count of boards it passes on is the witness: the same under B = 129 and
-    200 (split 128), more than under B = 0 or 300 (split 256).  Decided boards equal their known
-    solutions; budget hits come back as their input."""
+    at 128, so no board is finished there past B nodes.  The split phase is one slot per board,
+    so the count of boards it passes on is the witness: about the same under B = 129 and 200 (split
+    128), several times more than under B = 0 or 300 (split 256; measured 1,661-1,665 against
+    191-194).  (Not exactly equal: solve4's node count for a board depends on the boards it shares a
+    wave with, see test_prop32_with_node_budget.)  Decided boards equal their known solutions;
+    budget hits come back as their input."""
     engine.set_option(L.SDK_OPT_PROP32, 1)
     boards, sol = synth.make_hard_sym(1 << 20, threads=8)
     passed = {}
@@ -191,7 +193,9 @@ def test_prop32_fallback_split_phase_within_node_budget(engine):
         if b == 0:
             assert (st == 1).all()
         passed[b] = engine.get_option(L.SDK_OPT_SPLIT_BOARDS)
-    assert passed[129] == passed[200] > passed[0] == passed[300], passed
+    assert abs(passed[129] - passed[200]) <= 0.02 * passed[200], passed
+    assert abs(passed[0] - passed[300]) <= 0.05 * passed[300] + 2, passed
+    assert passed[200] > 4 * passed[300], passed
 
 
 def test_prop32_not_used_without_locked_candidates_under_budget(engine):

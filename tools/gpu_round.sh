@@ -50,6 +50,13 @@ for s in $steps; do
         || { echo "pmc $c failed"; tail -20 "$out/pmc_$c.err"; exit 1; }
     done
     python3 tools/pmc_summary.py "$out" | tee "$out/pmc_summary.txt" ;;
+  hard_trace)   # the hard-search passes' dispatch sequence (prop32, split phase, donation, scatters)
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$root/$out/hard_trace" -o run --output-format csv \
+      -- python3 "$root/tools/hard_phases.py" ${HARD_ARGS:-} > "$root/$out/hard_phases.json" 2> "$root/$out/hard_phases.err") \
+      || { echo "hard trace failed"; tail -20 "$out/hard_phases.err"; exit 1; }
+    cat "$out/hard_phases.json"
+    python3 tools/hard_phases_summary.py "$out/hard_trace" > "$out/hard_phases_summary.txt"
+    head -3 "$out/hard_phases_summary.txt" ;;
   *) echo "unknown step $s"; exit 2 ;;
   esac
 done

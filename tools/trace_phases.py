@@ -1,4 +1,4 @@
-"""Per-dispatch kernel sequence of rocprofv3 kernel traces (dev tool for tools/gpu_r04h.sh).
+"""Per-dispatch kernel sequence of rocprofv3 kernel traces (dev tool; rocprofv3 --kernel-trace runs of tools/gpu_round.sh).
 
 usage: python3 tools/trace_phases.py <dir> <variant>...   (reads <dir>/<variant>/**/*kernel_trace.csv)
 Writes <dir>/phases_<variant>.txt (every dispatch: name, duration us, grid) and prints the

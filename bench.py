@@ -102,8 +102,10 @@ def parse_args():
     ap.add_argument("--c5-boards", default="15,14",
                     help="C5 boards: 16/15/14 clues (S1 with clues removed; counts 7,309 / 3,481,026 / 18,204,270); "
                          "the first is counted by the two-stage split, the second by the rebalanced one")
-    ap.add_argument("--first-boards", default="heaviest,S1,S2",
-                    help="first-solution leg (sharded_solve over all ranks): boards, heaviest or S1..S5 ('' = skip)")
+    ap.add_argument("--first-boards", default="heaviest,antibt,S1",
+                    help="first-solution leg (sharded_solve over all ranks): boards -- heaviest, antibt (the "
+                         "anti-backtracking 17-clue puzzle) or S1..S5 ('' = skip); each at the default frontier "
+                         "and split (4 boards per rank, 16-node rounds)")
     ap.add_argument("--frontier-probe", type=int, default=1_000_000,
                     help="boards of the timed one-board frontier build beside the rebalanced count (0 = skip)")
     ap.add_argument("--lane-puzzles", type=int, default=200_000,
@@ -461,8 +463,19 @@ def first_board(synth, name):
     if name == "heaviest":
         hp, hs = synth.make_hard_heaviest(1, threads=cpu_share())
         return hp[0], hs[0], "the committed hard set's heaviest puzzle"
+    if name == "antibt":
+        return (synth.parse(ANTI_BACKTRACKING), synth.parse(ANTI_BACKTRACKING_SOLUTION),
+                "the 17-clue puzzle built against brute-force backtracking (first row 987654321; "
+                "138,350,633 reference validations by the oracle's C port)")
     return (synth.parse(synth.SEEDS17[name]), synth.parse(synth.SEED_SOLUTIONS[name]),
             f"17-clue seed {name} (SURVEY App. A)")
+
+
+# Wikipedia "Sudoku solving algorithms": a puzzle built so that row-major ascending backtracking
+# needs as many steps as possible (its solution's first row is 987654321)
+ANTI_BACKTRACKING = "000000000000003085001020000000507000004000100090000000500000073002010000000040009"
+ANTI_BACKTRACKING_SOLUTION = ("987654321246173985351928746128537694634892157795461832519286473472319568"
+                              "863745219")
 
 
 def first_solution_leg(eng, d, args, synth):
@@ -474,25 +487,33 @@ def first_solution_leg(eng, d, args, synth):
     from distributed_sudoku_solver_amd.shard import RcclComm, sharded_solve
     comm = RcclComm(eng, d.rank, d.world, transport=d.comm) if d.world > 1 else None
     res, ok = {}, True
+    # each board twice: at the default frontier (CUs x waves x 8 boards per GPU: these boards are then
+    # usually decided inside the frontier build) and split -- a frontier of 4 boards per rank and a
+    # 16-node round budget, so the search runs in rounds, refines its heavy boards and (N > 1)
+    # rebalances by moving records: the collective path, on a one-board workload
+    cases = []
+    for name in args.first_boards.split(","):
+        cases += [(name, name, {}), (name + "_split", name, {"target": 4 * d.world, "round_budget": 16})]
     try:
-        for name in args.first_boards.split(","):
+        for key, name, kw in cases:
             board, sol, what = first_board(synth, name)
-            sharded_solve(eng, board, d.rank, d.world, comm=comm)      # warm-up
+            sharded_solve(eng, board, d.rank, d.world, comm=comm, **kw)      # warm-up
             best = None
             for _ in range(3):
                 info = {}
                 d.barrier()
                 t0 = time.perf_counter()
-                out, st = sharded_solve(eng, board, d.rank, d.world, comm=comm, info=info)
+                out, st = sharded_solve(eng, board, d.rank, d.world, comm=comm, info=info, **kw)
                 w = d.max(time.perf_counter() - t0)
                 good = st == 1 and bool(np.array_equal(np.asarray(out, np.uint8), sol))
                 ok &= good
                 if best is None or w < best[0]:
                     best = (w, info, good)
             w, info, good = best
-            res[name] = {"board": what, "wall_ms": 1000.0 * w, "ok": good, "rounds": info.get("rounds"),
-                         "moved_records": info.get("moved_records"), "refines": info.get("refines"),
-                         "steals": info.get("steals"), "frontier_boards": info.get("frontier")}
+            res[key] = {"board": what, "wall_ms": 1000.0 * w, "ok": good, "rounds": info.get("rounds"),
+                        "moved_records": info.get("moved_records"), "refines": info.get("refines"),
+                        "steals": info.get("steals"), "frontier_boards": info.get("frontier"),
+                        "target": kw.get("target", "default"), "round_budget": kw.get("round_budget", "default")}
     finally:
         if comm is not None:
             comm.close()

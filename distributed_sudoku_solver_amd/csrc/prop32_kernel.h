@@ -73,7 +73,8 @@ struct Prop32Args {
     uint32_t* heads;         // kP32Heads counters kP32HeadStride words apart (zeroed)
     uint32_t* list;          // [0] undecided boards, then their indices (list[0] zeroed)
     uint8_t* list_in;        // the undecided boards' inputs, dense, in list order
-    uint32_t lc_every;       // a locked-candidates pass every lc_every-th step
+    uint32_t lc_every;       // a locked-candidates pass after step lc_first, then every lc_every-th
+    uint32_t lc_first;       // step (lc_first = lc_every: after every lc_every-th step)
     uint32_t max_steps;      // boards still live after this many steps are undecided
     int handover;            // the list gets an undecided board's propagated grid (its closed cells
                              // filled in: the same completions) instead of its input; not for
@@ -722,6 +723,7 @@ __device__ __forceinline__ void prop32_body(Prop32Args a, uint64_t* stamps) {
         uint64_t undec = inert64 & valid, inexact = undec;
         uint64_t live = valid & ~undec, solved = 0ull, contra = 0ull, fixw = 0ull;
         bool lc = false;
+        uint32_t next_lc = a.lc_first;     // the step after which the next locked-candidates pass runs
 #if SDK_PROP32_STATS
         uint32_t st_lc = 0, st_t4 = ~0u, st_t1 = ~0u;
 #endif
@@ -780,9 +782,11 @@ __device__ __forceinline__ void prop32_body(Prop32Args a, uint64_t* stamps) {
                 }
             }
             __builtin_amdgcn_wave_barrier();
-            // every lc_every-th step is followed by a locked-candidates pass; that step also reports
-            // which boards it left unchanged (a board unchanged by it and by the pass is stuck)
-            lc = live != 0ull && (it % a.lc_every) == 0u;
+            // step lc_first and every lc_every-th after it are followed by a locked-candidates pass;
+            // that step also reports which boards it left unchanged (a board unchanged by it and by
+            // the pass is stuck)
+            lc = live != 0ull && it == next_lc;
+            if (lc) next_lc += a.lc_every;
             if (lc) {
                 const uint32_t chg_own = p32_cells<true>(w, x);
                 fixw = live & ~p32_mask64(p32_half_or(w.act ? chg_own : 0u));

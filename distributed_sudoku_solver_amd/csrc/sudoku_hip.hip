@@ -359,7 +359,9 @@ struct sdk_ctx {
     uint64_t split_big = 0;        // the phased solve being enqueued: its split budget above
                                    // sdk::kBudgetBigBoards searched boards (device-counted batches)
     int prop32 = 1;                // QUAD: bit-sliced root propagation first (SDK_OPT_PROP32)
-    int prop32_lc = 4;             // ... a locked-candidates pass every this many steps
+    int prop32_lc = 5 | (3 << 8);  // ... a locked-candidates pass every this many steps (low byte),
+                                   //     the first after step (value >> 8), 0 = the period: after
+                                   //     steps 3, 8, 13, ... (prop32 "schedule")
     int64_t prop32_min = 4096;     // ... for batches of at least this many boards
     int prop32_handover = 1;       // ... undecided boards searched from their propagated grids
     int prop32_tail_live = 0;      // ... a group's last (at most this many) live boards handed over
@@ -870,7 +872,8 @@ int launch_prop32_solve(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, int8_t*
     a.heads = static_cast<uint32_t*>(c->p32_ctl.p);
     a.list = static_cast<uint32_t*>(c->p32_list.p);
     a.list_in = static_cast<uint8_t*>(c->p32_in.p);
-    a.lc_every = (uint32_t)std::max(1, c->prop32_lc);
+    a.lc_every = (uint32_t)std::max(1, c->prop32_lc & 0xFF);
+    a.lc_first = (c->prop32_lc >> 8) ? (uint32_t)(c->prop32_lc >> 8) : a.lc_every;
     a.max_steps = 96;
     // the search continues from the propagated grids when no node budget applies (a budget counts
     // nodes from the input, so the statuses of budget hits would differ)
@@ -1347,7 +1350,8 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             c->prop32 = (int)value;
             return SDK_OK;
         case SDK_OPT_PROP32_LC:
-            if (value < 1 || value > 64) return fail(SDK_EINVAL, "SDK_OPT_PROP32_LC out of range 1..64");
+            if ((value & 0xFF) < 1 || (value & 0xFF) > 64 || (value >> 8) > 64)
+                return fail(SDK_EINVAL, "SDK_OPT_PROP32_LC: period 1..64 | first step 0..64 << 8");
             c->prop32_lc = (int)value;
             return SDK_OK;
         case SDK_OPT_PROP32_MIN:

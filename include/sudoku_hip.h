@@ -122,7 +122,9 @@ extern "C" {
                                  /* does not decide are searched by solve4 and scattered */
                                  /* back -- same answers and statuses.  Plain solves     */
                                  /* only (no masks, work counters or strided inputs)     */
-#define SDK_OPT_PROP32_LC    26  /* ... a locked-candidates pass every N steps (default 4) */
+#define SDK_OPT_PROP32_LC    26  /* ... a locked-candidates pass every N steps (low byte),  */
+                                 /* the first after step F (N | F << 8; F = 0: after step */
+                                 /* N); default 5 | 3 << 8: after steps 3, 8, 13, ...     */
 #define SDK_OPT_PROP32_MIN   27  /* ... for batches of at least N boards (default 4096)   */
 #define SDK_OPT_PROP32_UNDECIDED 28 /* read-only: boards the last solve's propagation pass */
                                  /* left to the search (waits)                           */

@@ -253,7 +253,7 @@ class BenchStubEngine(OracleEngine):
         self._comm.allgather(send, recv, nbytes)
 
     def comm_p2p(self, ops):
-        self._comm.p2p([(k, p, b.data if hasattr(b, "data") else b, n) for k, p, b, n in ops])
+        self._comm.p2p([(k, p, b.data if isinstance(b, _HostBuffer) else b, n) for k, p, b, n in ops])
 
     def alloc(self, nbytes):
         return _HostBuffer(nbytes)

@@ -85,7 +85,7 @@ def test_bench_gpus2_first_solution_leg(tmp_path):
     assert leg["ok"] is True and leg["S4"]["ok"] is True, leg
     for key in ("wall_ms", "rounds", "moved_records", "refines", "steals", "frontier_boards"):
         assert leg["S4"][key] is not None, key
-    assert leg["S4"]["rounds"] >= 1
+    assert leg["S4"]["rounds"] >= 1 and leg["S4_split"]["ok"] is True and leg["S4_split"]["refines"] >= 1
 
 
 def test_no_torch_blocker_works(tmp_path):

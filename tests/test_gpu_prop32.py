@@ -214,3 +214,24 @@ def test_prop32_not_used_without_locked_candidates_under_budget(engine):
             assert np.array_equal(out[st == 1], sol[st == 1])
     finally:
         engine.set_option(L.SDK_OPT_LOCKED, 1)
+
+
+@pytest.mark.parametrize("lc", [4, 5 | (3 << 8), 1, 7 | (1 << 8), 64])
+def test_prop32_lc_schedules_same_answers(engine, lc):
+    """Round 6: the locked-candidates schedule (SDK_OPT_PROP32_LC = period | first step << 8) only
+    changes when the pass runs, never an answer: every schedule gives the search-only boards and
+    statuses on the edge batch and minimal puzzles."""
+    boards = np.concatenate([edge_boards(2048, seed=17), synth.make_minimal_sym(4096, seed=19, threads=8)[0]])
+    try:
+        (o1, s1), (o0, s0) = _both(engine, boards, SDK_OPT_PROP32_LC=lc)
+    finally:
+        engine.set_option(L.SDK_OPT_PROP32_LC, 5 | (3 << 8))
+    assert np.array_equal(s1, s0) and np.array_equal(o1, o0)
+
+
+def test_prop32_lc_option_encoding(engine):
+    assert engine.get_option(L.SDK_OPT_PROP32_LC) == 5 | (3 << 8)          # the default schedule
+    for bad in (0, 65, 5 | (65 << 8), 3 << 8):
+        with pytest.raises(Exception):
+            engine.set_option(L.SDK_OPT_PROP32_LC, bad)
+    assert engine.get_option(L.SDK_OPT_PROP32_LC) == 5 | (3 << 8)

@@ -57,6 +57,9 @@ for s in $steps; do
     cat "$out/hard_phases.json"
     python3 tools/hard_phases_summary.py "$out/hard_trace" > "$out/hard_phases_summary.txt"
     head -3 "$out/hard_phases_summary.txt" ;;
+  ab)   # option settings / library variants (tools/ab_opts.sh; SETTINGS, VARIANTS, WORKLOADS, REPS from the env)
+    bash tools/ab_opts.sh > "$out/ab.log" 2>&1 || { echo "ab failed"; tail -20 "$out/ab.log"; exit 1; }
+    cat "$out/ab.log" ;;
   *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -60,6 +60,15 @@ for s in $steps; do
   ab)   # option settings / library variants (tools/ab_opts.sh; SETTINGS, VARIANTS, WORKLOADS, REPS from the env)
     bash tools/ab_opts.sh > "$out/ab.log" 2>&1 || { echo "ab failed"; tail -20 "$out/ab.log"; exit 1; }
     cat "$out/ab.log" ;;
+  read_ceiling)   # HBM read ceiling for the checker's access pattern (tools/read_ceiling.hip)
+    timeout -k 10 120 tools/read_ceiling > "$out/read_ceiling.txt" 2>&1 || { echo "read ceiling failed"; tail -5 "$out/read_ceiling.txt"; exit 1; }
+    cat "$out/read_ceiling.txt" ;;
+  pmc_pipe)   # per-SIMD pipe and LDS counters of the C4 launch and the hard_1m one-launch solve
+    bash tools/pmc_r04.sh "$out/pmc_pipe" c4 hard1m > "$out/pmc_pipe.log" 2>&1 || { echo "pmc pipe failed"; tail -10 "$out/pmc_pipe.log"; exit 1; }
+    tail -5 "$out/pmc_pipe.log" ;;
+  pmc_c4)   # FETCH/WRITE/SQ passes of the C4 and C3 launches (tools/pmc_c4.sh)
+    bash tools/pmc_c4.sh "$out/pmc_c4" > "$out/pmc_c4.log" 2>&1 || { echo "pmc c4 failed"; tail -10 "$out/pmc_c4.log"; exit 1; }
+    tail -5 "$out/pmc_c4.log" ;;
   *) echo "unknown step $s"; exit 2 ;;
   esac
 done

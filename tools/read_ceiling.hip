@@ -1,0 +1,86 @@
+// read_ceiling.hip -- HBM read ceiling of this GPU for the checker's access pattern (dev tool).
+//
+// The checker (check_kernel.h) streams 81 B per board and writes 1 B: it is a READ stream.  The
+// guide's 6.29 TB/s is a float4 COPY (half of it writes).  This measures what a pure read stream
+// reaches -- dwordx4 loads, grid-stride, U loads in flight per thread, an XOR fold and one dword
+// store per thread -- over the checker's 8.1 GB, with and without the non-temporal hint, at the
+// checker's grid (blocks of 256 threads, B blocks per CU), so the checker's fraction of 8 TB/s can
+// be read against the fraction a plain read reaches.
+//
+// build: hipcc -O3 --offload-arch=gfx950 -o tools/read_ceiling tools/read_ceiling.hip
+// run:   tools/read_ceiling [bytes=8100000000]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_kernel(const u32x4* __restrict__ src, size_t n4, unsigned* __restrict__ out) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(&src[i + u * stride]) : src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u];
+    }
+    for (; i < n4; i += stride) acc ^= src[i];
+    out[(size_t)blockIdx.x * blockDim.x + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+
+#define CK(x)                                                                           \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) {                                                         \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                \
+            return 1;                                                                   \
+        }                                                                               \
+    } while (0)
+
+template <int U, bool NT>
+int run(const char* name, const u32x4* src, size_t n4, unsigned* out, int cus, int bpc) {
+    const unsigned grid = (unsigned)(cus * bpc);
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int w = 0; w < 10; ++w) read_kernel<U, NT><<<grid, 256>>>(src, n4, out);
+    CK(hipDeviceSynchronize());
+    const int reps = 20;
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) read_kernel<U, NT><<<grid, 256>>>(src, n4, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= reps;
+    const double tbs = (double)n4 * 16 / (ms * 1e-3) / 1e12;
+    std::printf("%-8s U=%d blocks/CU=%2d  %.3f ms  %.3f TB/s  %.1f %% of 8 TB/s\n", name, U, bpc, ms, tbs, tbs / 8.0 * 100);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    const size_t bytes = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 8100000000ull;
+    const size_t n4 = bytes / 16;
+    hipDeviceProp_t p;
+    CK(hipGetDeviceProperties(&p, 0));
+    const int cus = p.multiProcessorCount;
+    u32x4* src;
+    unsigned* out;
+    CK(hipMalloc(&src, n4 * 16));
+    CK(hipMemset(src, 0x5a, n4 * 16));
+    CK(hipMalloc(&out, (size_t)cus * 16 * 256 * 4));
+    std::printf("read ceiling: %.2f GB, %d CUs\n", n4 * 16 / 1e9, cus);
+    for (int bpc : {3, 4, 8}) {
+        if (run<4, true>("nt", src, n4, out, cus, bpc) || run<4, false>("plain", src, n4, out, cus, bpc) ||
+            run<8, true>("nt", src, n4, out, cus, bpc))
+            return 1;
+    }
+    CK(hipFree(src));
+    CK(hipFree(out));
+    return 0;
+}

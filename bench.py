@@ -70,6 +70,9 @@ def parse_args():
     ap.add_argument("--check-steps", type=int, default=20)
     ap.add_argument("--check-warmup", type=int, default=10,
                     help="untimed checker launches first (the memory clocks ramp under sustained streaming)")
+    ap.add_argument("--warm-ms", type=float, default=60.0,
+                    help="untimed warm-up: beyond the W steps, passes back to back until this long (ms) -- the "
+                         "GPU's clock ramps over its first ~40 ms of load (profiles/r06/clock_ramp_r06i.jsonl)")
     ap.add_argument("--order", choices=["mrv_unique", "lex"], default="lex")
     ap.add_argument("--solver", choices=sorted(SOLVERS), default="quad",
                     help="solve kernel: four boards per wave (solve4_kernel), two (solve2_kernel) or one (solve_kernel)")
@@ -343,8 +346,7 @@ def c2_leg(eng, d, args, synth):
     p, sol = synth.make_30clue(n, seed=args.seed + 31, lo=d.rank * n)
     d_in, d_out, d_st = eng.alloc(n * 81), eng.alloc(n * 81), eng.alloc(n)
     d_in.upload(p)
-    eng.solve_batch_dev(d_in, d_out, d_st, n)
-    eng.synchronize()
+    _warm(args, [eng], lambda e, k: e.solve_batch_dev(d_in, d_out, d_st, n))
     eng.timer_reset()
     d.barrier()
     t0 = time.perf_counter()
@@ -543,7 +545,21 @@ def minimal_leg(eng, d, args, synth, L):
             "search": stats, "parity": {"mismatched_boards": bad, "checked_boards": d.world * n}}
 
 
-def _timed_solves(eng, d, p, s, steps, contexts=1):
+def _warm(args, engines, launch, at_least=1):
+    """Untimed passes before a timed region: at least one per engine context, then on, back to back,
+    until --warm-ms of load (the GPU's clock ramps over its first ~40 ms of load)."""
+    t_w, i = time.perf_counter(), 0
+    while i < max(at_least, len(engines)) or (time.perf_counter() - t_w) * 1000.0 < args.warm_ms:
+        k = i % len(engines)
+        launch(engines[k], k)
+        engines[k].synchronize()
+        i += 1
+    for e in engines:
+        e.synchronize()
+    return i
+
+
+def _timed_solves(eng, d, p, s, steps, args, contexts=1):
     """Wall time of `steps` solve_batch_dev passes over resident boards (+ 1 warm-up per context),
     max over ranks; every board of every output buffer checked against its known answer afterwards.
     contexts > 1: consecutive passes on that many engine contexts in turn (own stream and output
@@ -554,10 +570,7 @@ def _timed_solves(eng, d, p, s, steps, contexts=1):
     d_in = eng.alloc(n * 81)
     bufs = [(e.alloc(n * 81), e.alloc(n)) for e in engines]
     d_in.upload(p)
-    for e, (d_out, d_st) in zip(engines, bufs):
-        e.solve_batch_dev(d_in, d_out, d_st, n)
-    for e in engines:
-        e.synchronize()
+    _warm(args, engines, lambda e, k: e.solve_batch_dev(d_in, bufs[k][0], bufs[k][1], n))
     d.barrier()
     t0 = time.perf_counter()
     for i in range(steps):
@@ -627,7 +640,7 @@ def hard_leg(eng, d, args, synth, L):
             eng.set_option(L.SDK_OPT_ORDER, order)
             eng.set_option(L.SDK_OPT_DONATE, dn)
             eng.set_option(L.SDK_OPT_DONATE_MAX, 0)       # phased at any size (hard_1m is above the default)
-            el, b = _timed_solves(eng, d, bp, bs, 6 if ctx > 1 else 5, contexts=ctx)
+            el, b = _timed_solves(eng, d, bp, bs, 6 if ctx > 1 else 5, args, contexts=ctx)
             bad += b
             checked += d.world * len(bp) * ctx
             legs[mode] = {"value": d.world * len(bp) / el, "unit": "puzzles/s", "ms": el * 1000.0, "contexts": ctx,
@@ -878,9 +891,16 @@ def solve_leg(eng, d, args, puzzles, expected, steps, warmup, contexts=1, timed=
     d_in = eng.alloc(max(n, 1) * 81)
     outs = [(e.alloc(max(n, 1) * 81), e.alloc(max(n, 1))) for e in engines]
     d_in.upload(puzzles)
-    for i in range(max(warmup, nctx)):
+    # untimed: W passes, and on until the GPU has run passes back to back for --warm-ms (its clock
+    # ramps from ~1.9 to ~2.35 GHz over the first ~40 ms of load, profiles/r06/clock_ramp_r06i.jsonl)
+    t_w, i = time.perf_counter(), 0
+    while i < max(warmup, nctx) or (time.perf_counter() - t_w) * 1000.0 < args.warm_ms:
         o, st = outs[i % nctx]
         engines[i % nctx].solve_batch_dev(d_in, o, st, n)
+        if i >= max(warmup, nctx) - 1:
+            engines[i % nctx].synchronize()       # paces the time-based part
+        i += 1
+    solve_leg.warm_passes = i
     for e in engines:
         e.synchronize()
         if timed:          # per-launch HIP events (the roofline's kernel time); off: wall clock only
@@ -979,8 +999,12 @@ def main():
         # tile the pool through HBM (content repeats; every byte is still streamed from HBM)
         for s in range(0, nb, pool_n):
             d_b.upload(pool[:min(pool_n, nb - s)], offset=s * 81)
-        for _ in range(max(1, args.check_warmup)):
+        t_w, cw = time.perf_counter(), 0
+        while cw < max(1, args.check_warmup) or (time.perf_counter() - t_w) * 1000.0 < args.warm_ms:
             eng.check_batch_dev(d_b, d_v, nb)
+            if cw >= max(1, args.check_warmup) - 1:
+                eng.synchronize()
+            cw += 1
         eng.synchronize()
         eng.timer_reset()
         d.barrier()
@@ -1015,6 +1039,7 @@ def main():
                          "traffic_note": crec.get("traffic_note") if crec else None,
                          "kernel": "sdk::check_kernel"},
             "parity": {"mismatched_boards": cbad, "checked_boards": d.world * nb},
+            "warm_launches": cw,
         }
         if d.rank == 0 and d.world == 1 and args.cpu_seconds > 0:
             checker_leg["cpu_baseline"] = cpu_baseline_check(pool[:1_000_000], min(5.0, args.cpu_seconds),
@@ -1034,6 +1059,7 @@ def main():
     single_stream = {"value": total * args.steps / s_el, "unit": "puzzles/s", "ms_per_step": s_el / args.steps * 1e3,
                      "avg_kernel_ms": avg_kernel_s * 1e3, "contexts": 1,
                      "avg_fallback_ms": solve_leg.fallback_ms, "clock": solve_leg.clock,
+                     "warm_passes": solve_leg.warm_passes,
                      "parity": {"mismatched_boards": bad_total, "checked_boards": total}}
     inflight = max(1, args.inflight)
     if inflight > 1:
@@ -1156,6 +1182,10 @@ def main():
             "solver": args.solver,
             "parallelism": f"batch-shard x{d.world} (contiguous slices, no collectives)",
             "passes_in_flight_per_gpu": inflight,
+            "warmup_policy": (f"W = {args.warmup} untimed passes, continued back to back until {args.warm_ms:g} ms "
+                              "of load before each timed region (the clock ramps from ~1.9 to ~2.35 GHz over "
+                              "the first ~40 ms; profiles/r06/clock_ramp_r06i.jsonl); exactly `steps` passes "
+                              "timed"),
         },
         "single_stream": single_stream,
         "roofline": roofline,

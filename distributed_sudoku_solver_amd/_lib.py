@@ -62,6 +62,8 @@ SDK_CHECK_REG2 = 1
 SDK_CHECK_GLDS2 = 2
 SDK_CHECK_GLDS3 = 3
 SDK_CHECK_GLDS4 = 4
+SDK_CHECK_WAVE1 = 5
+SDK_CHECK_WAVE2 = 6
 
 SDK_SOLVER_WAVE = 0
 SDK_SOLVER_HALFWAVE = 1

@@ -278,6 +278,67 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel_glds(const uint8_t
     wait_vmcnt<0>();
 }
 
+// Variant: per-WAVE tiles, no workgroup barrier (round 6).  Each wave streams its own 64-board
+// tiles (5,184 B = 324 x 16 B: 5 dwordx4 per lane, a 6th for lanes 0..3) through its own LDS
+// region; a wave's LDS accesses execute in issue order, so the stores of a tile and the lanes'
+// re-aligning reads need no barrier, and no wave waits for another's loads (the workgroup barrier
+// of check_kernel makes each tile's next loads wait for the slowest wave of four).  NBUF register
+// sets keep NBUF tiles of the wave in flight: the loads of tile i + NBUF are issued as soon as tile
+// i is in LDS, before its boards are checked.  Tiles are dealt grid-stride by global wave index.
+constexpr int kCheckWaveTileVec = 64 * 81 / 16;          // 324 x uint4 per wave tile
+template <int NBUF>
+__global__ __launch_bounds__(kCheckThreads) void check_kernel_wave(const uint8_t* __restrict__ boards,
+                                                                   uint8_t* __restrict__ verdict, uint64_t n) {
+    // +16 B per wave region: the last lane's 22nd dword read runs one dword past its tile
+    __shared__ __attribute__((aligned(16))) u32x4 tiles[(kCheckThreads / 64) * (kCheckWaveTileVec + 1)];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    u32x4* my = tiles + wv * (kCheckWaveTileVec + 1);
+    const uint64_t nw = (uint64_t)gridDim.x * (kCheckThreads / 64);
+    const uint64_t nfull = n / 64;                              // full wave tiles
+    const uint64_t ntiles = (n + 63) / 64;
+    uint64_t tix = (uint64_t)blockIdx.x * (kCheckThreads / 64) + wv;
+    u32x4 ring[NBUF][6];
+    auto load = [&](uint64_t ti, u32x4 (&r)[6]) {
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(boards + ti * (64 * 81));
+#pragma unroll
+        for (int j = 0; j < 5; ++j) r[j] = __builtin_nontemporal_load(&s4[j * 64 + lane]);
+        if (lane < 4) r[5] = __builtin_nontemporal_load(&s4[5 * 64 + lane]);
+    };
+#pragma unroll
+    for (int b = 0; b < NBUF; ++b)
+        if (tix + b * nw < nfull) load(tix + b * nw, ring[b]);
+    for (int b = 0; tix < ntiles; tix += nw) {
+        const uint64_t base = tix * 64;
+        if (tix < nfull) {
+#pragma unroll
+            for (int k = 0; k < NBUF; ++k) {          // the ring slot as a compile-time index
+                if (k == b) {
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) my[j * 64 + lane] = ring[k][j];
+                    if (lane < 4) my[5 * 64 + lane] = ring[k][5];
+                    __builtin_amdgcn_wave_barrier();
+                    const uint64_t nxt = tix + NBUF * nw;
+                    if (nxt < nfull) load(nxt, ring[k]);   // in flight while this tile is checked
+                }
+            }
+        } else {
+            // ragged last tile: each lane copies its own record byte by byte
+            const uint64_t cnt = n - base;
+            uint8_t* tb = reinterpret_cast<uint8_t*>(my);
+            if ((uint64_t)lane < cnt) {
+                const uint8_t* src = boards + (base + lane) * 81;
+#pragma unroll
+                for (int k = 0; k < 81; ++k) tb[81 * lane + k] = src[k];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (base + lane < n) verdict[base + lane] = check_board_lds(reinterpret_cast<const uint32_t*>(my), lane);
+        __builtin_amdgcn_wave_barrier();              // every lane's reads before the next stores
+        b = (b + 1 == NBUF) ? 0 : b + 1;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // check_kernel_i64 -- the same literal rule on int64 cells, for boards whose values
 // leave 0..255 (the reference takes any Python int; JSON numbers reach it unchanged).

@@ -462,6 +462,8 @@ int launch_check(sdk_ctx* c, const uint8_t* d_in, uint8_t* d_out, size_t n) {
         case SDK_CHECK_GLDS2: sdk::check_kernel_glds<2><<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
         case SDK_CHECK_GLDS3: sdk::check_kernel_glds<3><<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
         case SDK_CHECK_GLDS4: sdk::check_kernel_glds<4><<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
+        case SDK_CHECK_WAVE1: sdk::check_kernel_wave<1><<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
+        case SDK_CHECK_WAVE2: sdk::check_kernel_wave<2><<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
         default: sdk::check_kernel<<<grid, sdk::kCheckThreads, 0, c->stream>>>(d_in, d_out, (uint64_t)n); break;
     }
     HIPCALL(hipGetLastError());
@@ -1372,7 +1374,7 @@ int sdk_set_option(sdk_ctx* c, int key, int64_t value) {
             c->xcd_heads = (int)value;
             return SDK_OK;
         case SDK_OPT_CHECK_VARIANT:
-            if (value < SDK_CHECK_REG1 || value > SDK_CHECK_GLDS4) return fail(SDK_EINVAL, "bad check variant %lld", (long long)value);
+            if (value < SDK_CHECK_REG1 || value > SDK_CHECK_WAVE2) return fail(SDK_EINVAL, "bad check variant %lld", (long long)value);
             c->check_variant = (int)value;
             return SDK_OK;
         default:

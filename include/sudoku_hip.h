@@ -140,6 +140,8 @@ extern "C" {
 #define SDK_CHECK_GLDS2      2  /* LDS-DMA ring of 2 tiles (check_kernel_glds<2>)      */
 #define SDK_CHECK_GLDS3      3  /* LDS-DMA ring of 3 tiles (check_kernel_glds<3>)      */
 #define SDK_CHECK_GLDS4      4  /* LDS-DMA ring of 4 tiles (check_kernel_glds<4>)      */
+#define SDK_CHECK_WAVE1      5  /* per-wave 64-board tiles, no barrier, 1 ahead       */
+#define SDK_CHECK_WAVE2      6  /* ... 2 tiles ahead per wave (check_kernel_wave<2>)   */
 
 #define SDK_SOLVER_WAVE      0  /* one board per wavefront (solve_kernel)              */
 #define SDK_SOLVER_HALFWAVE  1  /* two boards per wavefront, 27 lanes x 3 cells each   */

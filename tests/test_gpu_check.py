@@ -60,7 +60,8 @@ def test_empty_batch(engine):
     assert engine.check_batch(np.zeros((0, 81), np.uint8)).shape == (0,)
 
 
-VARIANTS = [L.SDK_CHECK_REG1, L.SDK_CHECK_REG2, L.SDK_CHECK_GLDS2, L.SDK_CHECK_GLDS3, L.SDK_CHECK_GLDS4]
+VARIANTS = [L.SDK_CHECK_REG1, L.SDK_CHECK_REG2, L.SDK_CHECK_GLDS2, L.SDK_CHECK_GLDS3, L.SDK_CHECK_GLDS4,
+            L.SDK_CHECK_WAVE1, L.SDK_CHECK_WAVE2]
 
 
 @pytest.mark.parametrize("variant", VARIANTS)

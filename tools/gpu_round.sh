@@ -69,6 +69,10 @@ for s in $steps; do
   pmc_c4)   # FETCH/WRITE/SQ passes of the C4 and C3 launches (tools/pmc_c4.sh)
     bash tools/pmc_c4.sh "$out/pmc_c4" > "$out/pmc_c4.log" 2>&1 || { echo "pmc c4 failed"; tail -10 "$out/pmc_c4.log"; exit 1; }
     tail -5 "$out/pmc_c4.log" ;;
+  clock_ramp)   # per-pass kernel time and in-kernel clock of C4 from a cold GPU (tools/clock_ramp.py)
+    timeout -k 10 180 python -u tools/clock_ramp.py > "$out/clock_ramp.jsonl" 2> "$out/clock_ramp.err" \
+      || { echo "clock ramp failed"; tail -10 "$out/clock_ramp.err"; exit 1; }
+    cat "$out/clock_ramp.jsonl" ;;
   *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -17,9 +17,14 @@ for s in range(0, nb, pool_n):
     L.check(eng.lib.sdk_memcpy_h2d(eng.ctx, ctypes.c_void_p(d_b.ptr.value + s * 81), ctypes.c_void_p(b.ctypes.data), m * 81), "h2d")
 expect = np.tile(exp, nb // pool_n + 1)[:nb]
 names = {L.SDK_CHECK_REG1: "reg1", L.SDK_CHECK_REG2: "reg2", L.SDK_CHECK_GLDS2: "glds2",
-         L.SDK_CHECK_GLDS3: "glds3", L.SDK_CHECK_GLDS4: "glds4"}
+         L.SDK_CHECK_GLDS3: "glds3", L.SDK_CHECK_GLDS4: "glds4", L.SDK_CHECK_WAVE1: "wave1",
+         L.SDK_CHECK_WAVE2: "wave2"}
 grid = {L.SDK_CHECK_REG1: (2, 3, 4), L.SDK_CHECK_REG2: (2, 3), L.SDK_CHECK_GLDS2: (2, 3),
-        L.SDK_CHECK_GLDS3: (1, 2), L.SDK_CHECK_GLDS4: (1,)}
+        L.SDK_CHECK_GLDS3: (1, 2), L.SDK_CHECK_GLDS4: (1,), L.SDK_CHECK_WAVE1: (2, 3, 4),
+        L.SDK_CHECK_WAVE2: (2, 3, 4)}
+only = os.environ.get("SWEEP_VARIANTS")          # e.g. "reg1,wave1,wave2"
+if only:
+    grid = {k: v for k, v in grid.items() if names[k] in only.split(",")}
 res = {}
 v = np.empty(nb, np.uint8)
 for rnd in range(3):

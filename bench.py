@@ -115,12 +115,12 @@ def parse_args():
                     help="per-lane reference-DFS leg on a C2 prefix (rank 0, N=1; 0 = skip)")
     ap.add_argument("--leg-timeout", type=float, default=120.0,
                     help="watchdog for the side legs: print what was measured and exit")
-    ap.add_argument("--pmc-pipe", default=os.path.join(ROOT, "profiles", "r05", "pmc_pipe.json"),
+    ap.add_argument("--pmc-pipe", default=os.path.join(ROOT, "profiles", "r06", "pmc_pipe.json"),
                     help="per-SIMD pipe counters of the solve kernel (tools/pmc_r04.sh; '' = none)")
     ap.add_argument("--issue-calib", default=os.path.join(ROOT, "profiles", "r05", "issue_calib_pmc.json"),
                     help="VALU issue ceilings of the solve kernel's instruction mix (tools/issue_calib.hip under "
                          "rocprofv3, tools/issue_calib_summary.py; '' = none)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r05", "pmc_c4.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r06", "pmc_c4.json"),
                     help="per-launch PMC figures of the C4 solve kernel and the C3 checker from rocprofv3 passes "
                          "of this bench at its default sizes (tools/pmc_c4.sh); '' = report traffic null")
     ap.add_argument("--engine-factory", default="", help=argparse.SUPPRESS)

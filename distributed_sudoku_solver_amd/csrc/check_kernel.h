@@ -24,6 +24,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef SDK_CHECK_FAST_OR
+#define SDK_CHECK_FAST_OR 0
+#endif
+
 namespace sdk {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -48,17 +52,29 @@ __device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int 
     for (int k = 0; k < 21; ++k) w[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh);
     w[20] &= 0xFFu;  // only cell 80 belongs to this board
 
+#if SDK_CHECK_FAST_OR
+    // Fast path when every byte is < 32 (one OR over the record, no per-byte test): 1 << v is then
+    // exact.  A byte in 10..31 sets a bit >= 10 in its row's sum, so such a board leaves for the exact
+    // path below after the sums (so can a row whose duplicates carry past bit 9 -- correct there too).
+    uint32_t orall = 0;
+#pragma unroll
+    for (int k = 0; k < 21; ++k) orall |= w[k];
+    const bool small = (orall & 0xE0E0E0E0u) == 0u;
+#else
     // any byte >= 10 ?  ((b & 0x7F) + 0x76) sets bit 7 iff (b & 0x7F) >= 10, no carry out of the byte
     uint32_t big = 0;
 #pragma unroll
     for (int k = 0; k < 21; ++k) big |= (((w[k] & 0x7F7F7F7Fu) + 0x76767676u) | w[k]) & 0x80808080u;
+    const bool small = big == 0;
+#endif
 
     uint32_t rowacc[9], colacc[9], boxacc[9];
 #pragma unroll
     for (int u = 0; u < 9; ++u) rowacc[u] = colacc[u] = boxacc[u] = 0;
     uint32_t box00 = 0;
-    uint8_t verdict;
-    if (big == 0) {
+    uint8_t verdict = 0;
+    bool exact = !small;
+    if (small) {
 #pragma unroll
         for (int k = 0; k < 81; ++k) {
             const int r = k / 9, c = k % 9, b = (r / 3) * 3 + c / 3;
@@ -67,6 +83,19 @@ __device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int 
             rowacc[r] += p; colacc[c] += p; boxacc[b] += p;
             if (b == 0) box00 += v;
         }
+#if SDK_CHECK_FAST_OR
+        uint32_t rsum = 0, bad = 0;
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+            rsum |= rowacc[u];
+            bad |= (rowacc[u] ^ 0x3FEu) | ((colacc[u] ^ 0x3FEu) << 16);
+        }
+        uint32_t badb = 0;
+#pragma unroll
+        for (int u = 0; u < 9; ++u) badb |= boxacc[u] ^ 0x3FEu;
+        exact = (rsum & ~0x3FFu) != 0u;       // a byte in 10..31 (or a carried duplicate): exact path
+        const bool rows = (bad & 0xFFFFu) == 0u, cols = (bad >> 16) == 0u, boxes = badb == 0u;
+#else
         bool rows = true, cols = true, boxes = true;
 #pragma unroll
         for (int u = 0; u < 9; ++u) {
@@ -74,9 +103,14 @@ __device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int 
             cols &= colacc[u] == 0x3FEu;
             boxes &= boxacc[u] == 0x3FEu;
         }
+#endif
         verdict = (uint8_t)((rows && cols && boxes) ? 1u : 0u);
         if (rows && cols && box00 == 45u) verdict |= 2u;
-    } else {
+    }
+    if (exact) {
+        box00 = 0;
+#pragma unroll
+        for (int u = 0; u < 9; ++u) rowacc[u] = colacc[u] = boxacc[u] = 0;
 #pragma unroll
         for (int k = 0; k < 81; ++k) {
             const int r = k / 9, c = k % 9, b = (r / 3) * 3 + c / 3;

@@ -235,3 +235,25 @@ def test_prop32_lc_option_encoding(engine):
         with pytest.raises(Exception):
             engine.set_option(L.SDK_OPT_PROP32_LC, bad)
     assert engine.get_option(L.SDK_OPT_PROP32_LC) == 5 | (3 << 8)
+
+
+def test_prop32_clock_twin_same_answers_and_plausible_clock(engine):
+    """The stamped twin of the pass (sdk_debug_clock_arm, the bench's live clock for roofline.valu)
+    gives the same boards and statuses as the pass itself, and its stamps a clock inside the card's
+    range (MI355X: at most 2.4 GHz)."""
+    import ctypes
+    lib = engine.lib
+    engine.set_option(L.SDK_OPT_PROP32, 1)
+    boards = np.concatenate([edge_boards(2048, seed=23), synth.make_17clue(8192, seed=29)[0]])
+    out0, st0, _ = engine.solve_batch(boards)
+    assert lib.sdk_debug_clock_arm(engine.ctx, 1) == 0
+    try:
+        out1, st1, _ = engine.solve_batch(boards)
+        out4 = (ctypes.c_double * 4)()
+        wgs = ctypes.c_int64()
+        assert lib.sdk_debug_clock_read(engine.ctx, out4, ctypes.byref(wgs)) == 0
+    finally:
+        lib.sdk_debug_clock_arm(engine.ctx, 0)
+    assert np.array_equal(st0, st1) and np.array_equal(out0, out1)
+    assert wgs.value > 0
+    assert 0.5 < out4[1] <= out4[0] <= out4[2] < 2.6, list(out4)

@@ -33,6 +33,42 @@ __global__ __launch_bounds__(256) void read_kernel(const u32x4* __restrict__ src
     out[(size_t)blockIdx.x * blockDim.x + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
 }
 
+// the checker's access pattern without its arithmetic: a 256-board tile (20,736 B) per workgroup,
+// grid-stride over tiles, the next tile's six dwordx4 per thread in flight while the current one
+// goes through LDS (stores, barrier, one dword read per thread, barrier) -- check_kernel minus
+// check_board_lds.  SPIN adds ~SPIN dependent VALU per tile and thread, standing in for the check.
+template <int SPIN>
+__global__ __launch_bounds__(256) void tile_kernel(const u32x4* __restrict__ src, size_t ntiles, unsigned* __restrict__ out) {
+    __shared__ u32x4 tile[1296 + 1];
+    const int t = threadIdx.x;
+    u32x4 pre[6];
+    unsigned acc = 0;
+    size_t tix = blockIdx.x;
+    auto load = [&](size_t ti) {
+        const u32x4* s4 = src + ti * 1296;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) pre[j] = __builtin_nontemporal_load(&s4[j * 256 + t]);
+        if (t < 16) pre[5] = __builtin_nontemporal_load(&s4[5 * 256 + t]);
+    };
+    if (tix < ntiles) load(tix);
+    for (; tix < ntiles; tix += gridDim.x) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) tile[j * 256 + t] = pre[j];
+        if (t < 16) tile[5 * 256 + t] = pre[5];
+        __syncthreads();
+        if (tix + gridDim.x < ntiles) load(tix + gridDim.x);
+        unsigned v = reinterpret_cast<const unsigned*>(tile)[(t * 81) >> 2];
+#pragma unroll 1
+        for (int k = 0; k < SPIN; ++k) v = v * 2654435761u + (unsigned)k;
+        acc ^= v;
+        __syncthreads();
+    }
+    out[blockIdx.x * 256 + t] = acc;
+}
+
+template <int SPIN>
+int run_tile(const u32x4* src, size_t n4, unsigned* out, int cus, int bpc);
+
 #define CK(x)                                                                           \
     do {                                                                                \
         hipError_t e_ = (x);                                                            \
@@ -63,6 +99,29 @@ int run(const char* name, const u32x4* src, size_t n4, unsigned* out, int cus, i
     return 0;
 }
 
+template <int SPIN>
+int run_tile(const u32x4* src, size_t n4, unsigned* out, int cus, int bpc) {
+    const unsigned grid = (unsigned)(cus * bpc);
+    const size_t ntiles = n4 / 1296;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int w = 0; w < 10; ++w) tile_kernel<SPIN><<<grid, 256>>>(src, ntiles, out);
+    CK(hipDeviceSynchronize());
+    const int reps = 20;
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) tile_kernel<SPIN><<<grid, 256>>>(src, ntiles, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= reps;
+    const double tbs = (double)ntiles * 1296 * 16 / (ms * 1e-3) / 1e12;
+    std::printf("tile     spin=%3d blocks/CU=%2d  %.3f ms  %.3f TB/s  %.1f %% of 8 TB/s\n", SPIN, bpc, ms, tbs,
+                tbs / 8.0 * 100);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const size_t bytes = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 8100000000ull;
     const size_t n4 = bytes / 16;
@@ -75,6 +134,11 @@ int main(int argc, char** argv) {
     CK(hipMemset(src, 0x5a, n4 * 16));
     CK(hipMalloc(&out, (size_t)cus * 16 * 256 * 4));
     std::printf("read ceiling: %.2f GB, %d CUs\n", n4 * 16 / 1e9, cus);
+    for (int bpc : {3, 4}) {
+        if (run_tile<0>(src, n4, out, cus, bpc) || run_tile<100>(src, n4, out, cus, bpc) ||
+            run_tile<300>(src, n4, out, cus, bpc))
+            return 1;
+    }
     for (int bpc : {3, 4, 8}) {
         if (run<4, true>("nt", src, n4, out, cus, bpc) || run<4, false>("plain", src, n4, out, cus, bpc) ||
             run<8, true>("nt", src, n4, out, cus, bpc))

@@ -27,6 +27,9 @@
 #ifndef SDK_CHECK_FAST_OR
 #define SDK_CHECK_FAST_OR 0
 #endif
+#ifndef SDK_CHECK_NT_STORE
+#define SDK_CHECK_NT_STORE 0
+#endif
 
 namespace sdk {
 
@@ -38,6 +41,14 @@ constexpr int kCheckTileVec = kCheckTileBytes / 16;          // 1296 x uint4
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[21], int k) {
     return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+}
+
+// the verdict byte; with SDK_CHECK_NT_STORE a non-temporal store (the stream's only writes)
+__device__ __forceinline__ void put_verdict(uint8_t* p, uint8_t v) {
+    if (SDK_CHECK_NT_STORE)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
 }
 
 __device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int t) {
@@ -54,8 +65,8 @@ __device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int 
 
 #if SDK_CHECK_FAST_OR
     // Fast path when every byte is < 32 (one OR over the record, no per-byte test): 1 << v is then
-    // exact.  A byte in 10..31 sets a bit >= 10 in its row's sum, so such a board leaves for the exact
-    // path below after the sums (so can a row whose duplicates carry past bit 9 -- correct there too).
+    // exact, and a byte in 10..31 shows as a bit >= 10 in the OR of the one-hot terms (an OR: no
+    // carries), so such a board leaves for the exact path below after the sums.
     uint32_t orall = 0;
 #pragma unroll
     for (int k = 0; k < 21; ++k) orall |= w[k];
@@ -72,6 +83,7 @@ __device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int 
 #pragma unroll
     for (int u = 0; u < 9; ++u) rowacc[u] = colacc[u] = boxacc[u] = 0;
     uint32_t box00 = 0;
+    [[maybe_unused]] uint32_t allor = 0;
     uint8_t verdict = 0;
     bool exact = !small;
     if (small) {
@@ -81,19 +93,17 @@ __device__ __forceinline__ uint8_t check_board_lds(const uint32_t* tile_dw, int 
             const uint32_t v = byte_of(w, k);
             const uint32_t p = 1u << v;
             rowacc[r] += p; colacc[c] += p; boxacc[b] += p;
+            if (SDK_CHECK_FAST_OR) allor |= p;
             if (b == 0) box00 += v;
         }
 #if SDK_CHECK_FAST_OR
-        uint32_t rsum = 0, bad = 0;
+        uint32_t bad = 0;
 #pragma unroll
-        for (int u = 0; u < 9; ++u) {
-            rsum |= rowacc[u];
-            bad |= (rowacc[u] ^ 0x3FEu) | ((colacc[u] ^ 0x3FEu) << 16);
-        }
+        for (int u = 0; u < 9; ++u) bad |= (rowacc[u] ^ 0x3FEu) | ((colacc[u] ^ 0x3FEu) << 16);
         uint32_t badb = 0;
 #pragma unroll
         for (int u = 0; u < 9; ++u) badb |= boxacc[u] ^ 0x3FEu;
-        exact = (rsum & ~0x3FFu) != 0u;       // a byte in 10..31 (or a carried duplicate): exact path
+        exact = (allor & ~0x3FFu) != 0u;      // a byte in 10..31: the exact path
         const bool rows = (bad & 0xFFFFu) == 0u, cols = (bad >> 16) == 0u, boxes = badb == 0u;
 #else
         bool rows = true, cols = true, boxes = true;
@@ -174,7 +184,7 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel(const uint8_t* __r
         const uint64_t nxt = tix + gridDim.x;
         if (nxt < nfull) load_tile(nxt);                   // in flight during validation
         if ((uint64_t)t < cnt)
-            verdict[base + t] = check_board_lds(reinterpret_cast<const uint32_t*>(tile), t);
+            put_verdict(verdict + base + t, check_board_lds(reinterpret_cast<const uint32_t*>(tile), t));
         __syncthreads();
     }
 }
@@ -221,7 +231,7 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel_rr2(const uint8_t*
         __syncthreads();
         load_tile(tix + 2 * G, cur);
         if ((uint64_t)t < cnt)
-            verdict[base + t] = check_board_lds(reinterpret_cast<const uint32_t*>(tile), t);
+            put_verdict(verdict + base + t, check_board_lds(reinterpret_cast<const uint32_t*>(tile), t));
         __syncthreads();
     };
     uint64_t tix = blockIdx.x;
@@ -304,7 +314,7 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel_glds(const uint8_t
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's ds_writes (ragged path) landed
         __builtin_amdgcn_s_barrier();
         if ((uint64_t)t < cnt)
-            verdict[base + t] = check_board_lds(reinterpret_cast<const uint32_t*>(cur), t);
+            put_verdict(verdict + base + t, check_board_lds(reinterpret_cast<const uint32_t*>(cur), t));
         __builtin_amdgcn_s_waitcnt(0xc07f);   // this wave's ds_reads of cur are done
         __builtin_amdgcn_s_barrier();         // nobody reads cur when the next iteration refills it
         buf = (buf + 1 == NBUF) ? 0 : buf + 1;
@@ -367,7 +377,7 @@ __global__ __launch_bounds__(kCheckThreads) void check_kernel_wave(const uint8_t
             }
             __builtin_amdgcn_wave_barrier();
         }
-        if (base + lane < n) verdict[base + lane] = check_board_lds(reinterpret_cast<const uint32_t*>(my), lane);
+        if (base + lane < n) put_verdict(verdict + base + lane, check_board_lds(reinterpret_cast<const uint32_t*>(my), lane));
         __builtin_amdgcn_wave_barrier();              // every lane's reads before the next stores
         b = (b + 1 == NBUF) ? 0 : b + 1;
     }

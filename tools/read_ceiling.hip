@@ -37,9 +37,11 @@ __global__ __launch_bounds__(256) void read_kernel(const u32x4* __restrict__ src
 // grid-stride over tiles, the next tile's six dwordx4 per thread in flight while the current one
 // goes through LDS (stores, barrier, one dword read per thread, barrier) -- check_kernel minus
 // check_board_lds.  SPIN adds ~SPIN dependent VALU per tile and thread, standing in for the check.
-template <int SPIN>
-__global__ __launch_bounds__(256) void tile_kernel(const u32x4* __restrict__ src, size_t ntiles, unsigned* __restrict__ out) {
+template <int SPIN, int READS = 0, int STORE = 0>
+__global__ __launch_bounds__(256) void tile_kernel(const u32x4* __restrict__ src, size_t ntiles, unsigned* __restrict__ out,
+                                                   unsigned char* __restrict__ bytes = nullptr) {
     __shared__ u32x4 tile[1296 + 1];
+    __shared__ u32x4 vst[16];          // STORE 2: the tile's 256 verdict bytes
     const int t = threadIdx.x;
     u32x4 pre[6];
     unsigned acc = 0;
@@ -58,16 +60,25 @@ __global__ __launch_bounds__(256) void tile_kernel(const u32x4* __restrict__ src
         __syncthreads();
         if (tix + gridDim.x < ntiles) load(tix + gridDim.x);
         unsigned v = reinterpret_cast<const unsigned*>(tile)[(t * 81) >> 2];
+#pragma unroll
+        for (int k = 1; k < READS; ++k) v ^= reinterpret_cast<const unsigned*>(tile)[((t * 81) >> 2) + k];
 #pragma unroll 1
         for (int k = 0; k < SPIN; ++k) v = v * 2654435761u + (unsigned)k;
         acc ^= v;
+        if (STORE == 1) bytes[tix * 256 + t] = (unsigned char)v;
+        if (STORE == 3) __builtin_nontemporal_store((unsigned char)v, &bytes[tix * 256 + t]);
+        if (STORE == 2) {               // through LDS: one 16-B store per lane of the first 16 lanes
+            reinterpret_cast<unsigned char*>(vst)[t] = (unsigned char)v;
+            __syncthreads();
+            if (t < 16) reinterpret_cast<u32x4*>(bytes + tix * 256)[t] = vst[t];
+        }
         __syncthreads();
     }
     out[blockIdx.x * 256 + t] = acc;
 }
 
-template <int SPIN>
-int run_tile(const u32x4* src, size_t n4, unsigned* out, int cus, int bpc);
+template <int SPIN, int READS = 0, int STORE = 0>
+int run_tile(const u32x4* src, size_t n4, unsigned* out, int cus, int bpc, unsigned char* bytes = nullptr);
 
 #define CK(x)                                                                           \
     do {                                                                                \
@@ -99,26 +110,26 @@ int run(const char* name, const u32x4* src, size_t n4, unsigned* out, int cus, i
     return 0;
 }
 
-template <int SPIN>
-int run_tile(const u32x4* src, size_t n4, unsigned* out, int cus, int bpc) {
+template <int SPIN, int READS, int STORE>
+int run_tile(const u32x4* src, size_t n4, unsigned* out, int cus, int bpc, unsigned char* bytes) {
     const unsigned grid = (unsigned)(cus * bpc);
     const size_t ntiles = n4 / 1296;
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int w = 0; w < 10; ++w) tile_kernel<SPIN><<<grid, 256>>>(src, ntiles, out);
+    for (int w = 0; w < 10; ++w) tile_kernel<SPIN, READS, STORE><<<grid, 256>>>(src, ntiles, out, bytes);
     CK(hipDeviceSynchronize());
     const int reps = 20;
     CK(hipEventRecord(a));
-    for (int r = 0; r < reps; ++r) tile_kernel<SPIN><<<grid, 256>>>(src, ntiles, out);
+    for (int r = 0; r < reps; ++r) tile_kernel<SPIN, READS, STORE><<<grid, 256>>>(src, ntiles, out, bytes);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms = 0.f;
     CK(hipEventElapsedTime(&ms, a, b));
     ms /= reps;
     const double tbs = (double)ntiles * 1296 * 16 / (ms * 1e-3) / 1e12;
-    std::printf("tile     spin=%3d blocks/CU=%2d  %.3f ms  %.3f TB/s  %.1f %% of 8 TB/s\n", SPIN, bpc, ms, tbs,
-                tbs / 8.0 * 100);
+    std::printf("tile     spin=%3d reads=%2d store=%d blocks/CU=%2d  %.3f ms  %.3f TB/s  %.1f %% of 8 TB/s\n", SPIN,
+                READS, (int)STORE, bpc, ms, tbs, tbs / 8.0 * 100);
     return 0;
 }
 
@@ -134,11 +145,15 @@ int main(int argc, char** argv) {
     CK(hipMemset(src, 0x5a, n4 * 16));
     CK(hipMalloc(&out, (size_t)cus * 16 * 256 * 4));
     std::printf("read ceiling: %.2f GB, %d CUs\n", n4 * 16 / 1e9, cus);
+    unsigned char* vbytes;
+    CK(hipMalloc(&vbytes, n4 * 16 / 81 + 4096));
     for (int bpc : {3, 4}) {
-        if (run_tile<0>(src, n4, out, cus, bpc) || run_tile<100>(src, n4, out, cus, bpc) ||
-            run_tile<300>(src, n4, out, cus, bpc))
+        if (run_tile<0>(src, n4, out, cus, bpc) || run_tile<0, 22>(src, n4, out, cus, bpc) ||
+            run_tile<0, 22, 1>(src, n4, out, cus, bpc, vbytes) || run_tile<0, 22, 2>(src, n4, out, cus, bpc, vbytes) ||
+            run_tile<0, 22, 3>(src, n4, out, cus, bpc, vbytes) || run_tile<100>(src, n4, out, cus, bpc))
             return 1;
     }
+    CK(hipFree(vbytes));
     for (int bpc : {3, 4, 8}) {
         if (run<4, true>("nt", src, n4, out, cus, bpc) || run<4, false>("plain", src, n4, out, cus, bpc) ||
             run<8, true>("nt", src, n4, out, cus, bpc))

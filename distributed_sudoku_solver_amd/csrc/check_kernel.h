@@ -24,11 +24,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Round 6 (checker): the fast path is entered on one OR over the record (every byte < 32)
+// and left for the exact path on the OR of the one-hot terms (a byte in 10..31), and the verdicts
+// are non-temporal stores: 1.364 ms per 100M boards against 1.392 on one box (0 to fall back)
 #ifndef SDK_CHECK_FAST_OR
-#define SDK_CHECK_FAST_OR 0
+#define SDK_CHECK_FAST_OR 1
 #endif
 #ifndef SDK_CHECK_NT_STORE
-#define SDK_CHECK_NT_STORE 0
+#define SDK_CHECK_NT_STORE 1
 #endif
 
 namespace sdk {

@@ -46,6 +46,9 @@ __global__ __launch_bounds__(256) void tile_kernel(const u32x4* __restrict__ src
     u32x4 pre[6];
     unsigned acc = 0;
     size_t tix = blockIdx.x;
+    unsigned char pend[STORE >= 16 ? STORE : 1];
+    size_t ptix[STORE >= 16 ? STORE : 1];
+    unsigned npend = 0;
     auto load = [&](size_t ti) {
         const u32x4* s4 = src + ti * 1296;
 #pragma unroll
@@ -67,6 +70,14 @@ __global__ __launch_bounds__(256) void tile_kernel(const u32x4* __restrict__ src
         acc ^= v;
         if (STORE == 1) bytes[tix * 256 + t] = (unsigned char)v;
         if (STORE == 3) __builtin_nontemporal_store((unsigned char)v, &bytes[tix * 256 + t]);
+        if (STORE >= 16) {              // deferred: the last STORE tiles' bytes kept, then written in a burst
+            pend[npend % STORE] = (unsigned char)v;
+            ptix[npend % STORE] = tix;
+            if (++npend % STORE == 0) {
+#pragma unroll
+                for (int q = 0; q < STORE; ++q) __builtin_nontemporal_store(pend[q], &bytes[ptix[q] * 256 + t]);
+            }
+        }
         if (STORE == 2) {               // through LDS: one 16-B store per lane of the first 16 lanes
             reinterpret_cast<unsigned char*>(vst)[t] = (unsigned char)v;
             __syncthreads();
@@ -150,7 +161,8 @@ int main(int argc, char** argv) {
     for (int bpc : {3, 4}) {
         if (run_tile<0>(src, n4, out, cus, bpc) || run_tile<0, 22>(src, n4, out, cus, bpc) ||
             run_tile<0, 22, 1>(src, n4, out, cus, bpc, vbytes) || run_tile<0, 22, 2>(src, n4, out, cus, bpc, vbytes) ||
-            run_tile<0, 22, 3>(src, n4, out, cus, bpc, vbytes) || run_tile<100>(src, n4, out, cus, bpc))
+            run_tile<0, 22, 3>(src, n4, out, cus, bpc, vbytes) || run_tile<0, 22, 16>(src, n4, out, cus, bpc, vbytes) ||
+            run_tile<0, 22, 32>(src, n4, out, cus, bpc, vbytes) || run_tile<100>(src, n4, out, cus, bpc))
             return 1;
     }
     CK(hipFree(vbytes));

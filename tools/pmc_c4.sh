@@ -11,6 +11,8 @@ OFF="--c2-puzzles 0 --minimal-puzzles 0 --hard-leg 0 --count-leg 0 --lane-puzzle
 C4="$root/bench.py --steps 2 --warmup 1 --check-boards 0 $OFF"
 C3="$root/bench.py --steps 1 --warmup 0 --batch 1024 --check-boards 100000000 --check-steps 2 --check-warmup 1 $OFF"
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
+# stall attribution per wave-cycle (waiting on a counter / issue-stalled / issuing; LDS share)
+SQW="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM"
 run() {  # <tag> <counters> <program...>
   local tag=$1 ctr=$2; shift 2
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d "$root/$out/$tag" -o run -- "$@" \
@@ -22,6 +24,7 @@ run cal_write WRITE_SIZE "$root/tools/fetch_calib" 10000000
 run c4_fetch FETCH_SIZE python3 $C4
 run c4_write WRITE_SIZE python3 $C4
 run c4_sq "$SQ" python3 $C4
+run c4_sqw "$SQW" python3 $C4
 run c3_fetch FETCH_SIZE python3 $C3
 run c3_write WRITE_SIZE python3 $C3
 run c3_sq "$SQ" python3 $C3

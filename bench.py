@@ -117,7 +117,7 @@ def parse_args():
                     help="watchdog for the side legs: print what was measured and exit")
     ap.add_argument("--pmc-pipe", default=os.path.join(ROOT, "profiles", "r06", "pmc_pipe.json"),
                     help="per-SIMD pipe counters of the solve kernel (tools/pmc_r04.sh; '' = none)")
-    ap.add_argument("--issue-calib", default=os.path.join(ROOT, "profiles", "r05", "issue_calib_pmc.json"),
+    ap.add_argument("--issue-calib", default=os.path.join(ROOT, "profiles", "r06", "issue_calib_pmc.json"),
                     help="VALU issue ceilings of the solve kernel's instruction mix (tools/issue_calib.hip under "
                          "rocprofv3, tools/issue_calib_summary.py; '' = none)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r06", "pmc_c4.json"),
@@ -190,7 +190,7 @@ def mix_ceiling(path):
     with open(path) as f:
         recs = json.load(f)
     out = {}
-    for key in ("k_mix@8", "k_round<true>@8", "k_int2@8", "k_or3@8", "k_pk@8"):
+    for key in ("k_mix@8", "k_round<true>@8", "k_int2@8", "k_or3@8", "k_b3@8", "k_pk@8"):
         r = recs.get(key, {}).get("pipe")
         if r and r.get("valu_per_quad") is not None:
             out[key] = {"valu_per_quad": r["valu_per_quad"], "dual_frac": r.get("valu_dual_frac"),
@@ -1103,14 +1103,15 @@ def main():
         # THE CLOCK THE TIMED PASSES RAN AT (measured live in this run, kernel_clock; the profiled
         # run's clock is lower and would overstate every fraction), and beside it
         # at the 2.4 GHz cap.  Next to the peak: the ceiling this kernel's own instruction mix reaches
-        # on this GPU (tools/issue_calib.hip: 3-source VOP3 and packed VOP3P ops do not dual-issue,
-        # so the mix tops out near one per quad-cycle with every SIMD full)
+        # on this GPU (tools/issue_calib.hip under rocprofv3: legacy 3-source VOP3 ops -- v_or3,
+        # v_and_or -- and packed VOP3P ops do not dual-issue and top out near one per quad-cycle;
+        # v_bitop3 and 2-operand ops dual-issue, ~1.7 per quad-cycle with every SIMD full)
         rate = prec["valu_insts"] / avg_kernel_s
         mix = mix_ceiling(args.issue_calib)
-        # the kernel's own mix: prop32's step is 3-source VOP3 (v_bitop3 / v_or3) almost throughout --
-        # tools/issue_calib.hip k_or3; solve4's round is k_mix
+        # the kernel's own mix: prop32's step is v_bitop3 / 2-operand ops throughout since round 6
+        # (solve_kernel.h SDK_OR3) -- tools/issue_calib.hip k_b3; solve4's round is k_mix
         p32 = "prop32" in solve_kernel
-        mix_key = "k_or3@8" if p32 else "k_mix@8"
+        mix_key = "k_b3@8" if p32 else "k_mix@8"
         mix_q = (mix or {}).get(mix_key, {}).get("valu_per_quad")
 
         def priced(ghz):
@@ -1132,9 +1133,10 @@ def main():
             "at_2p4ghz_cap": cap,
             "mix_ceiling": ({"valu_per_quad": mix_q, "wave_instr_per_s": mix_q * 256 * at["clock_ghz"] * 1e9,
                              "frac": at["mix_ceiling_frac"], "calibration_kernel": mix_key,
-                             "note": ("tools/issue_calib.hip k_or3 (independent v_or3_b32 chains, ~4.4 waves per "
-                                      "SIMD): prop32's step is v_bitop3 / v_or3 throughout; 3-source VOP3 ops "
-                                      "dual-issue in ~7 % of quad-cycles (2-operand VOP2 ops: 78 %)" if p32 else
+                             "note": ("tools/issue_calib.hip k_b3 (independent v_bitop3_b32 chains, every SIMD "
+                                      "full): prop32's step is v_bitop3 and 2-operand ops throughout; they dual-"
+                                      "issue in ~79 % of quad-cycles (v_or3_b32 chains: 7 %, ~0.98 per quad-cycle, "
+                                      "k_or3@8 in the same calibration)" if p32 else
                                       "tools/issue_calib.hip k_mix at 8 waves/SIMD: the exact round's VALU "
                                       "(unit4x + 3 upd4x) on registers; VOP3 3-source and VOP3P packed ops "
                                       "dual-issue in ~7 % of quad-cycles (2-operand VOP2 ops: 78 %)"),

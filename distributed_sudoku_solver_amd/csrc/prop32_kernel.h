@@ -96,6 +96,18 @@ __device__ __forceinline__ uint32_t p32_half_or(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t p32_half_and(uint32_t x) { return ~p32_half_or(~x); }
 
+// one v_bitop3_b32 with truth table TT over (S0 = a, S1 = b, S2 = c).  Left to itself the compiler
+// forms three-input ORs as v_or3_b32, which issues at ~0.6x the rate of v_bitop3_b32
+// (solve_kernel.h SDK_OR3); the locked-candidates pass states its algebra through this.
+template <unsigned TT>
+__device__ __forceinline__ uint32_t p32_b3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(TT));
+    return r;
+}
+constexpr unsigned kB3Or3 = 0xFEu;       // S0 | S1 | S2
+constexpr unsigned kB3AndNor = 0x10u;    // S0 & ~(S1 | S2)
+
 // LDS access through address-space-3 pointers (ds_* instructions); loads are volatile so the
 // compiler keeps them single ds_read_b64 (a ds_read2_b64 pair costs 8 LDS-array cycles against
 // 2 x 2, MI355X_MICROARCH.md LDS table)
@@ -143,15 +155,15 @@ __device__ __forceinline__ void p32_singles(const P32Lane& w, P32Cells& x, uint3
         // instructions instead of the 17 of a one-word-at-a-time chain)
         const uint32_t* c = x.c[k];
         uint32_t o, w2, t1, t2, t3;
-        asm("v_or3_b32 %[o], %[c0], %[c1], %[c2]\n\t"
+        asm(SDK_OR3("%[o]", "%[c0]", "%[c1]", "%[c2]")
             "v_bitop3_b32 %[w], %[c0], %[c1], %[c2] bitop3:0xe8\n\t"
             "v_bitop3_b32 %[t1], %[o], %[c3], %[c4] bitop3:0xe8\n\t"
-            "v_or3_b32 %[o], %[o], %[c3], %[c4]\n\t"
+            SDK_OR3("%[o]", "%[o]", "%[c3]", "%[c4]")
             "v_bitop3_b32 %[t2], %[o], %[c5], %[c6] bitop3:0xe8\n\t"
-            "v_or3_b32 %[o], %[o], %[c5], %[c6]\n\t"
+            SDK_OR3("%[o]", "%[o]", "%[c5]", "%[c6]")
             "v_bitop3_b32 %[t3], %[o], %[c7], %[c8] bitop3:0xe8\n\t"
-            "v_or3_b32 %[o], %[o], %[c7], %[c8]\n\t"
-            "v_or3_b32 %[w], %[w], %[t1], %[t2]"
+            SDK_OR3("%[o]", "%[o]", "%[c7]", "%[c8]")
+            SDK_OR3("%[w]", "%[w]", "%[t1]", "%[t2]")
             : [o] "=&v"(o), [w] "=&v"(w2), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
             : [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [c4] "v"(c[4]), [c5] "v"(c[5]),
               [c6] "v"(c[6]), [c7] "v"(c[7]), [c8] "v"(c[8]));
@@ -180,7 +192,7 @@ __device__ __forceinline__ void p32_singles(const P32Lane& w, P32Cells& x, uint3
 //   unit, a pair:             twos |= maj(ones, a, b), ones |= a | b, T |= a&sa | b&sb (0xF8: S0 | S1&S2)
 __device__ __forceinline__ void p32_unit3(uint32_t& ones, uint32_t& twos, uint32_t& T, uint32_t a, uint32_t b,
                                           uint32_t c, uint32_t sa, uint32_t sb, uint32_t sc) {
-    asm("v_or3_b32 %[o], %[a], %[b], %[c]\n\t"
+    asm(SDK_OR3("%[o]", "%[a]", "%[b]", "%[c]")
         "v_bitop3_b32 %[w], %[a], %[b], %[c] bitop3:0xe8\n\t"
         "v_and_b32 %[t], %[a], %[sa]\n\t"
         "v_bitop3_b32 %[t], %[t], %[b], %[sb] bitop3:0xf8\n\t"
@@ -192,7 +204,7 @@ __device__ __forceinline__ void p32_unit2(uint32_t& ones, uint32_t& twos, uint32
                                           uint32_t sa, uint32_t sb) {
     uint32_t t;
     asm("v_bitop3_b32 %[t], %[o], %[a], %[b] bitop3:0xe8\n\t"
-        "v_or3_b32 %[o], %[o], %[a], %[b]\n\t"
+        SDK_OR3("%[o]", "%[o]", "%[a]", "%[b]")
         "v_or_b32 %[w], %[w], %[t]\n\t"
         "v_bitop3_b32 %[T], %[T], %[a], %[sa] bitop3:0xf8\n\t"
         "v_bitop3_b32 %[T], %[T], %[b], %[sb] bitop3:0xf8"
@@ -207,7 +219,7 @@ __device__ __forceinline__ void p32_upd1(uint32_t& c, uint32_t& H, uint32_t& any
                                          uint32_t cT, uint32_t rT, uint32_t bT, uint32_t cH, uint32_t rH, uint32_t bH) {
     uint32_t U, v;
     if (CHG)
-        asm("v_or3_b32 %[u], %[ct], %[rt], %[bt]\n\t"
+        asm(SDK_OR3("%[u]", "%[ct]", "%[rt]", "%[bt]")
             "v_bitop3_b32 %[h], %[ch], %[rh], %[bh] bitop3:0x7f\n\t"
             "v_bitop3_b32 %[v], %[c], %[u], %[s] bitop3:0xb0\n\t"
             "v_bitop3_b32 %[g], %[g], %[c], %[v] bitop3:0xf4\n\t"
@@ -216,7 +228,7 @@ __device__ __forceinline__ void p32_upd1(uint32_t& c, uint32_t& H, uint32_t& any
             : [c] "v"(c), [s] "v"(s), [ct] "v"(cT), [rt] "v"(rT), [bt] "v"(bT), [ch] "v"(cH), [rh] "v"(rH),
               [bh] "v"(bH));
     else
-        asm("v_or3_b32 %[u], %[ct], %[rt], %[bt]\n\t"
+        asm(SDK_OR3("%[u]", "%[ct]", "%[rt]", "%[bt]")
             "v_bitop3_b32 %[h], %[ch], %[rh], %[bh] bitop3:0x7f\n\t"
             "v_bitop3_b32 %[v], %[c], %[u], %[s] bitop3:0xb0\n\t"
             "v_bitop3_b32 %[a], %[a], %[v], %[h] bitop3:0xf8"
@@ -407,11 +419,14 @@ __device__ __forceinline__ void p32_elim(const P32Lane& w, uint32_t tl, uint32_t
                     l1b2 = p32_ld(w.reg, oL1B2 + 8 * h), l2b = p32_ld(w.reg, oL2B + 8 * h),
                     l2b1 = p32_ld(w.reg, oL2B1 + 8 * h), l2b2 = p32_ld(w.reg, oL2B2 + 8 * h),
                     lb1 = p32_ld(w.reg, oLB1 + 8 * h), lb2 = p32_ld(w.reg, oLB2 + 8 * h);
-        e[2 * h] = (l1b.x & ~(l1b1.x | l1b2.x)) | (l2b.x & ~(l2b1.x | l2b2.x)) |
-                   (lb1.x & ~(l1b1.x | l2b1.x)) | (lb2.x & ~(l1b2.x | l2b2.x));
+        e[2 * h] = p32_b3<kB3Or3>(p32_b3<kB3AndNor>(l1b.x, l1b1.x, l1b2.x), p32_b3<kB3AndNor>(l2b.x, l2b1.x, l2b2.x),
+                                  p32_b3<kB3AndNor>(lb1.x, l1b1.x, l2b1.x)) |
+                   p32_b3<kB3AndNor>(lb2.x, l1b2.x, l2b2.x);
         if (h < 4)
-            e[2 * h + 1] = (l1b.y & ~(l1b1.y | l1b2.y)) | (l2b.y & ~(l2b1.y | l2b2.y)) |
-                           (lb1.y & ~(l1b1.y | l2b1.y)) | (lb2.y & ~(l1b2.y | l2b2.y));
+            e[2 * h + 1] = p32_b3<kB3Or3>(p32_b3<kB3AndNor>(l1b.y, l1b1.y, l1b2.y),
+                                          p32_b3<kB3AndNor>(l2b.y, l2b1.y, l2b2.y),
+                                          p32_b3<kB3AndNor>(lb1.y, l1b1.y, l2b1.y)) |
+                           p32_b3<kB3AndNor>(lb2.y, l1b2.y, l2b2.y);
     }
 }
 
@@ -427,13 +442,13 @@ __device__ __forceinline__ uint32_t p32_locked(const P32Lane& w, P32Cells& x) {
     // presence of the lane's row triad (its own cells, closed ones included) and column triad
     uint32_t pr[9], pc[9];
 #pragma unroll
-    for (int d = 0; d < 9; ++d) pr[d] = x.c[0][d] | x.c[1][d] | x.c[2][d];
+    for (int d = 0; d < 9; ++d) pr[d] = p32_b3<kB3Or3>(x.c[0][d], x.c[1][d], x.c[2][d]);
 #pragma unroll
     for (int h = 0; h < 5; ++h) {
         const uint2 b0 = p32_ld(w.reg, ctri + 8 * h), b1 = p32_ld(w.reg, ctri + 360 + 8 * h),
                     b2 = p32_ld(w.reg, ctri + 720 + 8 * h);
-        pc[2 * h] = b0.x | b1.x | b2.x;
-        if (h < 4) pc[2 * h + 1] = b0.y | b1.y | b2.y;
+        pc[2 * h] = p32_b3<kB3Or3>(b0.x, b1.x, b2.x);
+        if (h < 4) pc[2 * h + 1] = p32_b3<kB3Or3>(b0.y, b1.y, b2.y);
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll

@@ -272,13 +272,13 @@ __device__ __forceinline__ void upd4(uint32_t& X, uint32_t& S, uint32_t U, uint3
         "v_pk_ashrrev_i16 %[t], 15, %[t] op_sel_hi:[0,1]\n\t"
         "v_bitop3_b32 %[v2], %[h], %[v1], %[t] bitop3:0xf4\n\t"
         "v_pk_add_u16 %[t], %[h], -1\n\t"
-        "v_and_or_b32 %[bm], %[h], %[t], %[bm]\n\t"
+        SDK_ANDOR("%[bm]", "%[h]", "%[t]", "%[bm]")
         "v_pk_add_u16 %[t], %[v2], -1\n\t"
         "v_and_b32 %[t], %[v2], %[t]\n\t"
         "v_or_b32 %[m], %[v2], %[s]\n\t"
         "v_pk_add_u16 %[t], %[t], -1\n\t"
         "v_pk_ashrrev_i16 %[t], 15, %[t] op_sel_hi:[0,1]\n\t"
-        "v_and_or_b32 %[s], %[v2], %[t], %[s]\n\t"
+        SDK_ANDOR("%[s]", "%[v2]", "%[t]", "%[s]")
         "v_bitop3_b32 %[xn], %[v2], %[t], %[t] bitop3:0x30\n\t"
         "v_bitop3_b32 %[chg], %[chg], %[x], %[xn] bitop3:0xf6"
         : [xn] "=&v"(xn), [v1] "=&v"(v1), [h] "=&v"(h), [t] "=&v"(t), [v2] "=&v"(v2), [m] "=&v"(m),
@@ -306,7 +306,7 @@ __device__ __forceinline__ void upd4x(uint32_t& X, uint32_t& S, uint32_t U, uint
         "v_and_b32 %[t], %[v2], %[t]\n\t"
         "v_pk_add_u16 %[t], %[t], -1\n\t"
         "v_pk_ashrrev_i16 %[t], 15, %[t] op_sel_hi:[0,1]\n\t"
-        "v_and_or_b32 %[s], %[v2], %[t], %[s]\n\t"
+        SDK_ANDOR("%[s]", "%[v2]", "%[t]", "%[s]")
         "v_bitop3_b32 %[xn], %[v2], %[t], %[t] bitop3:0x30\n\t"
         "v_bitop3_b32 %[chg], %[chg], %[x], %[xn] bitop3:0xf6"
         : [xn] "=&v"(xn), [v1] "=&v"(v1), [h] "=&v"(h), [t] "=&v"(t), [v2] "=&v"(v2),
@@ -324,26 +324,26 @@ __device__ __forceinline__ void upd4x(uint32_t& X, uint32_t& S, uint32_t U, uint
 __device__ __forceinline__ void unit4(const uint2 (&v)[9], uint32_t E, uint32_t Dn, uint32_t& once, uint32_t& T,
                                       uint32_t& bm) {
     uint32_t ox, os, t0, t1, t2, t3;
-    asm("v_or3_b32 %[ox], %[a0], %[a1], %[a2]\n\t"
+    asm(SDK_OR3("%[ox]", "%[a0]", "%[a1]", "%[a2]")
         "v_bitop3_b32 %[t0], %[a0], %[a1], %[a2] bitop3:0xe8\n\t"
         "v_bitop3_b32 %[t1], %[ox], %[a3], %[a4] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a3], %[a4]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a3]", "%[a4]")
         "v_bitop3_b32 %[t2], %[ox], %[a5], %[a6] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a5], %[a6]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a5]", "%[a6]")
         "v_bitop3_b32 %[t3], %[ox], %[a7], %[a8] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a7], %[a8]\n\t"
-        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a7]", "%[a8]")
+        SDK_OR3("%[t0]", "%[t0]", "%[t1]", "%[t2]")
         "v_bitop3_b32 %[t0], %[ox], %[t0], %[t3] bitop3:0x10\n\t"
         "v_and_b32 %[once], %[t0], %[e]\n\t"
-        "v_or3_b32 %[os], %[b0], %[b1], %[b2]\n\t"
+        SDK_OR3("%[os]", "%[b0]", "%[b1]", "%[b2]")
         "v_bitop3_b32 %[t0], %[b0], %[b1], %[b2] bitop3:0xe8\n\t"
         "v_bitop3_b32 %[t1], %[os], %[b3], %[b4] bitop3:0xe8\n\t"
-        "v_or3_b32 %[os], %[os], %[b3], %[b4]\n\t"
+        SDK_OR3("%[os]", "%[os]", "%[b3]", "%[b4]")
         "v_bitop3_b32 %[t2], %[os], %[b5], %[b6] bitop3:0xe8\n\t"
-        "v_or3_b32 %[os], %[os], %[b5], %[b6]\n\t"
+        SDK_OR3("%[os]", "%[os]", "%[b5]", "%[b6]")
         "v_bitop3_b32 %[t3], %[os], %[b7], %[b8] bitop3:0xe8\n\t"
-        "v_or3_b32 %[os], %[os], %[b7], %[b8]\n\t"
-        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        SDK_OR3("%[os]", "%[os]", "%[b7]", "%[b8]")
+        SDK_OR3("%[t0]", "%[t0]", "%[t1]", "%[t2]")
         "v_bitop3_b32 %[t0], %[t0], %[t3], %[dn] bitop3:0xa8\n\t"
         "v_bitop3_b32 %[t1], %[e], %[ox], %[os] bitop3:0x10\n\t"
         "v_or_b32 %[bm], %[t0], %[t1]\n\t"
@@ -378,25 +378,25 @@ __device__ __forceinline__ void unit4f(const uint2 (&v)[9], uint32_t& E, uint32_
     // as many temporaries as unit4 (its register budget): t1..t3 are reused once twice(S) is
     // formed (t1 = fresh mask, t2 = exact digits, t3 = dup), E and Dn are rewritten in place
     uint32_t ox, os, t0, t1, t2, t3;
-    asm("v_or3_b32 %[ox], %[a0], %[a1], %[a2]\n\t"
+    asm(SDK_OR3("%[ox]", "%[a0]", "%[a1]", "%[a2]")
         "v_bitop3_b32 %[t0], %[a0], %[a1], %[a2] bitop3:0xe8\n\t"
         "v_bitop3_b32 %[t1], %[ox], %[a3], %[a4] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a3], %[a4]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a3]", "%[a4]")
         "v_bitop3_b32 %[t2], %[ox], %[a5], %[a6] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a5], %[a6]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a5]", "%[a6]")
         "v_bitop3_b32 %[t3], %[ox], %[a7], %[a8] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a7], %[a8]\n\t"
-        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a7]", "%[a8]")
+        SDK_OR3("%[t0]", "%[t0]", "%[t1]", "%[t2]")
         "v_bitop3_b32 %[once], %[ox], %[t0], %[t3] bitop3:0x10\n\t"   // candidates in exactly one cell
-        "v_or3_b32 %[os], %[b0], %[b1], %[b2]\n\t"
+        SDK_OR3("%[os]", "%[b0]", "%[b1]", "%[b2]")
         "v_bitop3_b32 %[t0], %[b0], %[b1], %[b2] bitop3:0xe8\n\t"
         "v_bitop3_b32 %[t1], %[os], %[b3], %[b4] bitop3:0xe8\n\t"
-        "v_or3_b32 %[os], %[os], %[b3], %[b4]\n\t"
+        SDK_OR3("%[os]", "%[os]", "%[b3]", "%[b4]")
         "v_bitop3_b32 %[t2], %[os], %[b5], %[b6] bitop3:0xe8\n\t"
-        "v_or3_b32 %[os], %[os], %[b5], %[b6]\n\t"
+        SDK_OR3("%[os]", "%[os]", "%[b5]", "%[b6]")
         "v_bitop3_b32 %[t3], %[os], %[b7], %[b8] bitop3:0xe8\n\t"
-        "v_or3_b32 %[os], %[os], %[b7], %[b8]\n\t"
-        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        SDK_OR3("%[os]", "%[os]", "%[b7]", "%[b8]")
+        SDK_OR3("%[t0]", "%[t0]", "%[t1]", "%[t2]")
         "v_or_b32 %[t0], %[t0], %[t3]\n\t"                                // twice(S)
         "v_pk_ashrrev_i16 %[t1], 15, %[e] op_sel_hi:[0,1]\n\t"          // fm: 0xFFFF in fresh halves
         "v_and_b32 %[t2], 0x2000200, %[os]\n\t"                         // an inert given
@@ -441,21 +441,21 @@ __device__ __forceinline__ uint32_t lds_addr4(const void* p) {
 // cell closes -- and no completion is accepted or lost.
 __device__ __forceinline__ void unit4x(const uint2 (&v)[9], uint32_t E, uint32_t& once, uint32_t& T, uint32_t& bm) {
     uint32_t ox, os, t0, t1, t2, t3;
-    asm("v_or3_b32 %[ox], %[a0], %[a1], %[a2]\n\t"
+    asm(SDK_OR3("%[ox]", "%[a0]", "%[a1]", "%[a2]")
         "v_bitop3_b32 %[t0], %[a0], %[a1], %[a2] bitop3:0xe8\n\t"
         "v_bitop3_b32 %[t1], %[ox], %[a3], %[a4] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a3], %[a4]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a3]", "%[a4]")
         "v_bitop3_b32 %[t2], %[ox], %[a5], %[a6] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a5], %[a6]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a5]", "%[a6]")
         "v_bitop3_b32 %[t3], %[ox], %[a7], %[a8] bitop3:0xe8\n\t"
-        "v_or3_b32 %[ox], %[ox], %[a7], %[a8]\n\t"
-        "v_or3_b32 %[t0], %[t0], %[t1], %[t2]\n\t"
+        SDK_OR3("%[ox]", "%[ox]", "%[a7]", "%[a8]")
+        SDK_OR3("%[t0]", "%[t0]", "%[t1]", "%[t2]")
         "v_bitop3_b32 %[t0], %[ox], %[t0], %[t3] bitop3:0x10\n\t"
         "v_and_b32 %[once], %[t0], %[e]\n\t"
-        "v_or3_b32 %[os], %[b0], %[b1], %[b2]\n\t"
-        "v_or3_b32 %[os], %[os], %[b3], %[b4]\n\t"
-        "v_or3_b32 %[os], %[os], %[b5], %[b6]\n\t"
-        "v_or3_b32 %[os], %[os], %[b7], %[b8]\n\t"
+        SDK_OR3("%[os]", "%[b0]", "%[b1]", "%[b2]")
+        SDK_OR3("%[os]", "%[os]", "%[b3]", "%[b4]")
+        SDK_OR3("%[os]", "%[os]", "%[b5]", "%[b6]")
+        SDK_OR3("%[os]", "%[os]", "%[b7]", "%[b8]")
         "v_bitop3_b32 %[bm], %[e], %[ox], %[os] bitop3:0x10"
         : [ox] "=&v"(ox), [os] "=&v"(os), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
           [once] "=&v"(once), [bm] "=&v"(bm)

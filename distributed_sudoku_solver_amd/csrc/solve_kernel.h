@@ -44,6 +44,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Three-input OR and and-or in the kernels' inline asm.  v_or3_b32 and v_and_or_b32 (like every
+// older 3-source VOP3 op) issue at most ~1 per SIMD quad-cycle whatever the operands; the same
+// functions as v_bitop3_b32 truth tables (S0 | S1 | S2 = 0xFE, S0 & S1 | S2 = 0xEA) issue like
+// 2-operand ops -- ~1.55 per quad-cycle, 1.6x -- unless all three sources sit in one VGPR bank
+// (register index mod 4) (tools/bank_calib.hip, profiles/r06/bank_calib_r06x.txt).
+#ifndef SDK_BITOP3_OR
+#define SDK_BITOP3_OR 1
+#endif
+#if SDK_BITOP3_OR
+#define SDK_OR3(d, a, b, c) "v_bitop3_b32 " d ", " a ", " b ", " c " bitop3:0xfe\n\t"
+#define SDK_ANDOR(d, a, b, c) "v_bitop3_b32 " d ", " a ", " b ", " c " bitop3:0xea\n\t"
+#else
+#define SDK_OR3(d, a, b, c) "v_or3_b32 " d ", " a ", " b ", " c "\n\t"
+#define SDK_ANDOR(d, a, b, c) "v_and_or_b32 " d ", " a ", " b ", " c "\n\t"
+#endif
+
 namespace sdk {
 
 constexpr uint32_t kCands = 0x1FFu;

@@ -6,6 +6,7 @@
 // not from an instruction count by hand.
 //
 //   int2    8 independent chains of 2-operand 32-bit ops with inline constants (xor/add/and/or)
+//   b3      the or3 chains as v_bitop3_b32 only (round 6)
 //   or3     8 independent chains of 3-VGPR-source ops (v_or3_b32, v_bitop3_b32, v_and_or_b32):
 //           the unit summary's and the cell update's shape
 //   pk      8 independent chains of packed 16-bit ops (v_pk_add_u16, v_pk_ashrrev_i16,
@@ -74,6 +75,39 @@ __global__ __launch_bounds__(64) void k_or3(unsigned* out, unsigned seed, int it
             "v_and_or_b32 %0, %0, %8, %9\n v_and_or_b32 %1, %1, %8, %9\n v_and_or_b32 %2, %2, %8, %9\n"
             "v_and_or_b32 %3, %3, %8, %9\n v_and_or_b32 %4, %4, %8, %9\n v_and_or_b32 %5, %5, %8, %9\n"
             "v_and_or_b32 %6, %6, %8, %9\n v_and_or_b32 %7, %7, %8, %9\n"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "v"(k0), "v"(k1));
+    }
+    const unsigned r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+    if (r == 0x12345678u) out[blockIdx.x] = r + pad[0];
+}
+
+// the same chains as k_or3 with every op a v_bitop3_b32 (OR3 0xFE, XOR3 0x96, majority 0xE8,
+// and-or 0xEA): the form prop32's step and solve4's unit summary take since round 6
+// (solve_kernel.h SDK_OR3); operands where the compiler puts them, as in the kernels
+__global__ __launch_bounds__(64) void k_b3(unsigned* out, unsigned seed, int iters) {
+    extern __shared__ unsigned pad[];
+    unsigned a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+    unsigned a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    unsigned k0 = seed * 3u + threadIdx.x, k1 = seed ^ 0x5a5a5a5au;
+    for (int i = 0; i < iters; ++i) {
+        asm volatile(
+            "v_bitop3_b32 %0, %0, %8, %9 bitop3:0xfe\n v_bitop3_b32 %1, %1, %8, %9 bitop3:0xfe\n"
+            "v_bitop3_b32 %2, %2, %8, %9 bitop3:0xfe\n v_bitop3_b32 %3, %3, %8, %9 bitop3:0xfe\n"
+            "v_bitop3_b32 %4, %4, %8, %9 bitop3:0xfe\n v_bitop3_b32 %5, %5, %8, %9 bitop3:0xfe\n"
+            "v_bitop3_b32 %6, %6, %8, %9 bitop3:0xfe\n v_bitop3_b32 %7, %7, %8, %9 bitop3:0xfe\n"
+            "v_bitop3_b32 %0, %0, %8, %9 bitop3:0x96\n v_bitop3_b32 %1, %1, %8, %9 bitop3:0x96\n"
+            "v_bitop3_b32 %2, %2, %8, %9 bitop3:0x96\n v_bitop3_b32 %3, %3, %8, %9 bitop3:0x96\n"
+            "v_bitop3_b32 %4, %4, %8, %9 bitop3:0x96\n v_bitop3_b32 %5, %5, %8, %9 bitop3:0x96\n"
+            "v_bitop3_b32 %6, %6, %8, %9 bitop3:0x96\n v_bitop3_b32 %7, %7, %8, %9 bitop3:0x96\n"
+            "v_bitop3_b32 %0, %0, %8, %9 bitop3:0xe8\n v_bitop3_b32 %1, %1, %8, %9 bitop3:0xe8\n"
+            "v_bitop3_b32 %2, %2, %8, %9 bitop3:0xe8\n v_bitop3_b32 %3, %3, %8, %9 bitop3:0xe8\n"
+            "v_bitop3_b32 %4, %4, %8, %9 bitop3:0xe8\n v_bitop3_b32 %5, %5, %8, %9 bitop3:0xe8\n"
+            "v_bitop3_b32 %6, %6, %8, %9 bitop3:0xe8\n v_bitop3_b32 %7, %7, %8, %9 bitop3:0xe8\n"
+            "v_bitop3_b32 %0, %0, %8, %9 bitop3:0xea\n v_bitop3_b32 %1, %1, %8, %9 bitop3:0xea\n"
+            "v_bitop3_b32 %2, %2, %8, %9 bitop3:0xea\n v_bitop3_b32 %3, %3, %8, %9 bitop3:0xea\n"
+            "v_bitop3_b32 %4, %4, %8, %9 bitop3:0xea\n v_bitop3_b32 %5, %5, %8, %9 bitop3:0xea\n"
+            "v_bitop3_b32 %6, %6, %8, %9 bitop3:0xea\n v_bitop3_b32 %7, %7, %8, %9 bitop3:0xea\n"
             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
             : "v"(k0), "v"(k1));
     }
@@ -234,7 +268,7 @@ int main(int argc, char** argv) {
     };
     const K ks[] = {{"int2", 0, 32, 4096}, {"or3", 1, 32, 4096}, {"pk", 2, 32, 4096},
                     {"mix", 3, 0, 4096},   {"mix2", 4, 0, 2048}, {"round", 5, 0, 2048},
-                    {"roundf", 6, 0, 2048}};
+                    {"roundf", 6, 0, 2048}, {"b3", 7, 32, 4096}};
     for (int wps : {7, 8}) {
         const int per_cu = 4 * wps;
         const int blocks = dev_cus * per_cu;
@@ -252,6 +286,7 @@ int main(int argc, char** argv) {
                 case 4: k_mix2<<<blocks, 64, lds>>>(d, seed, k.iters); break;
                 case 5: k_round<true><<<blocks, 64, lds - 4200>>>(d, dboard, k.iters); break;
                 case 6: k_round<false><<<blocks, 64, lds - 4200>>>(d, dboard, k.iters); break;
+                case 7: k_b3<<<blocks, 64, lds>>>(d, seed, k.iters); break;
                 }
             };
             launch(7);

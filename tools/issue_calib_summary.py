@@ -15,7 +15,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_pipe_summary import _rows, _name, summarize  # noqa: E402
 
-KERNELS = ("k_int2", "k_or3", "k_pk", "k_mix2", "k_mix", "k_round<true>", "k_round<false>")
+KERNELS = ("k_int2", "k_or3", "k_b3", "k_pk", "k_mix2", "k_mix", "k_round<true>", "k_round<false>")
 
 
 def kernel_of(name):

@@ -121,8 +121,9 @@ __device__ __forceinline__ uint2 p32_lda(uint32_t addr) {   // an absolute LDS a
     const uint64_t v = *(const volatile __attribute__((address_space(3))) uint64_t*)(uintptr_t)addr;
     return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 }
+// stores volatile too: merged pairs become ds_write2_b64, 13 cycles against 2 x 6 (same table)
 __device__ __forceinline__ void p32_st(p32_lds_t* base, uint32_t off, uint32_t x, uint32_t y) {
-    *(__attribute__((address_space(3))) uint64_t*)(base + off) = (uint64_t)x | ((uint64_t)y << 32);
+    *(volatile __attribute__((address_space(3))) uint64_t*)(base + off) = (uint64_t)x | ((uint64_t)y << 32);
 }
 
 // a copy of v the compiler cannot see through: per-lane addresses derived from it are computed

@@ -511,13 +511,16 @@ __device__ __forceinline__ void round4(const Lane4& w, Cells4& c, uint32_t& bad,
         : "memory");
     asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(uc), "+v"(r0), "+v"(b0)::"memory");
     const uint32_t ucx = (uint32_t)uc, ucy = (uint32_t)(uc >> 32);
-    (EXACT ? upd4x : upd4)(c.x0, c.s0, ucx | (uint32_t)r0 | (uint32_t)b0, ucy | (uint32_t)(r0 >> 32) | (uint32_t)(b0 >> 32), bm, m0,
+    (EXACT ? upd4x : upd4)(c.x0, c.s0, sdk_or3(ucx, (uint32_t)r0, (uint32_t)b0),
+         sdk_or3(ucy, (uint32_t)(r0 >> 32), (uint32_t)(b0 >> 32)), bm, m0,
          chg);
     asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(r1), "+v"(b1), "+v"(c.x0), "+v"(c.s0)::"memory");
-    (EXACT ? upd4x : upd4)(c.x1, c.s1, ucx | (uint32_t)r1 | (uint32_t)b1, ucy | (uint32_t)(r1 >> 32) | (uint32_t)(b1 >> 32), bm, m1,
+    (EXACT ? upd4x : upd4)(c.x1, c.s1, sdk_or3(ucx, (uint32_t)r1, (uint32_t)b1),
+         sdk_or3(ucy, (uint32_t)(r1 >> 32), (uint32_t)(b1 >> 32)), bm, m1,
          chg);
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r2), "+v"(b2), "+v"(c.x1), "+v"(c.s1)::"memory");
-    (EXACT ? upd4x : upd4)(c.x2, c.s2, ucx | (uint32_t)r2 | (uint32_t)b2, ucy | (uint32_t)(r2 >> 32) | (uint32_t)(b2 >> 32), bm, m2,
+    (EXACT ? upd4x : upd4)(c.x2, c.s2, sdk_or3(ucx, (uint32_t)r2, (uint32_t)b2),
+         sdk_or3(ucy, (uint32_t)(r2 >> 32), (uint32_t)(b2 >> 32)), bm, m2,
          chg);
     // an open cell without candidates (a zero half of m0..m2); exact waves leave it to the
     // missing-digit test (upd4x)

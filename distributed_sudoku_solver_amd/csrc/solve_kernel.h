@@ -59,6 +59,12 @@
 #define SDK_OR3(d, a, b, c) "v_or3_b32 " d ", " a ", " b ", " c "\n\t"
 #define SDK_ANDOR(d, a, b, c) "v_and_or_b32 " d ", " a ", " b ", " c "\n\t"
 #endif
+// a | b | c as one SDK_OR3 (written in C, a three-input OR becomes v_or3_b32)
+__device__ __forceinline__ uint32_t sdk_or3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm(SDK_OR3("%0", "%1", "%2", "%3") : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 namespace sdk {
 

@@ -1090,8 +1090,9 @@ def main():
         "traffic_raw": srec.get("traffic_raw") if srec else None,
         "kernel": solve_kernel,
         "avg_kernel_ms": avg_kernel_s * 1000.0,
-        "note": "the kernel is bound by VALU issue (roofline.valu: against the 2-per-quad-cycle peak and the "
-                "ceiling of the kernel's own instruction mix); HBM fraction reported per contract (163 "
+        "note": "the kernel is bound by its LDS pipe (roofline.valu.pipe.lds_busy_frac, the stall counters in "
+                "roofline.valu.stalls; VALU issue against the 2-per-quad-cycle peak and the ceiling of the "
+                "kernel's own instruction mix in roofline.valu); HBM fraction reported per contract (163 "
                 "algorithmic B per puzzle)",
     }
     prec = pipe_record(args.pmc_pipe, "c4", n) if args.workload == "solve17" else None

@@ -57,12 +57,13 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="C4 headline: passes in flight per rank -- consecutive passes issued on this many engine "
                          "contexts in turn (own HIP stream, dequeue state and output buffer each), so one pass's "
                          "launch drain overlaps the next pass's start, as a serving node keeps batches in flight; "
                          "1 = one context.  The single-context figure and its per-launch kernel time (the "
-                         "roofline's) are reported beside it as `single_stream`")
+                         "roofline's) are reported beside it as `single_stream`.  2 since the round-6 kernels "
+                         "(1 / 2 / 3: 3.23-3.24 / 3.27-3.28 / 3.23-3.29 G/s, profiles/r06/ab_inflight_r06.log)")
     ap.add_argument("--workload", choices=["solve17", "solve30"], default="solve17")
     ap.add_argument("--batch", type=int, default=10_000_000, help="C4 puzzles, whole job (sharded over the GPUs)")
     ap.add_argument("--weak-leg", type=int, default=1, help="N > 1: also time --batch puzzles per GPU (weak scaling)")

@@ -53,8 +53,9 @@ def test_bench_gpus2_launches_two_ranks(tmp_path):
     assert r["n_gpus"] == 2 and r["scaling"] == "strong"
     assert r["config"]["puzzles_total"] == 301 and r["config"]["puzzles_per_gpu"] in (150, 151)
     # the single-context pass and every in-flight context's output are checked
-    assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 4 * 301}
-    assert r["config"]["passes_in_flight_per_gpu"] == 3 and r["single_stream"]["parity"]["mismatched_boards"] == 0
+    k = r["config"]["passes_in_flight_per_gpu"]
+    assert k == 2 and r["parity"] == {"mismatched_boards": 0, "checked_boards": (1 + k) * 301}
+    assert r["single_stream"]["parity"]["mismatched_boards"] == 0
     assert r["checker"]["parity"] == {"mismatched_boards": 0, "checked_boards": 4000}
     assert list(r)[-3:] == ["roofline_summary", "checker", "checker_summary"]   # the tail the driver keeps
     assert r["weak_scaling"]["parity"]["mismatched_boards"] == 0

@@ -65,7 +65,8 @@ def test_bench_gpus2_launches_two_ranks(tmp_path):
 def test_bench_gpus1_single_process(tmp_path):
     r = _run_bench(1, tmp=tmp_path)
     assert r["n_gpus"] == 1 and "weak_scaling" not in r
-    assert r["parity"] == {"mismatched_boards": 0, "checked_boards": 4 * 301}
+    k = r["config"]["passes_in_flight_per_gpu"]
+    assert r["parity"] == {"mismatched_boards": 0, "checked_boards": (1 + k) * 301}
 
 
 def test_bench_gpus2_count_legs_over_tcp_rccl_stub(tmp_path):

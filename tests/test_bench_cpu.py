@@ -98,3 +98,17 @@ def test_no_torch_blocker_works(tmp_path):
     env = dict(os.environ, PYTHONPATH=str(tmp_path))
     p = subprocess.run([sys.executable, "-c", "import torch"], env=env, capture_output=True, text=True)
     assert p.returncode != 0 and "must not import torch" in p.stderr
+
+
+def test_mix_ceiling_calibration_has_the_kernels_keys():
+    """The bench prices prop32 against k_b3 (its ORs are v_bitop3 since round 6) and solve4 against
+    k_mix; both come from the committed rocprofv3 calibration, and v_bitop3 chains pair (dual-issue)
+    where v_or3 chains do not."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    mix = bench.mix_ceiling(os.path.join(ROOT, "profiles", "r06", "issue_calib_pmc.json"))
+    assert mix and {"k_b3@8", "k_or3@8", "k_mix@8"} <= set(mix)
+    assert mix["k_b3@8"]["valu_per_quad"] > 1.5 * mix["k_or3@8"]["valu_per_quad"]
+    assert mix["k_b3@8"]["dual_frac"] > 0.5 > mix["k_or3@8"]["dual_frac"]

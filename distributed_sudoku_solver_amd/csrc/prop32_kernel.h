@@ -84,15 +84,25 @@ struct Prop32Args {
 };
 
 // OR / AND over the 32 lanes of each half, result in every lane of the half: rotations inside
-// each row of 16 (DPP), then lane ^ 16 (ds_swizzle, bit-mask mode: and 0x1F, xor 0x10).  Every
-// lane of the wave must be active.
+// each row of 16 (DPP), then the two rows of each half combined -- v_permlane16_swap (gfx950: the
+// odd rows of one register trade places with the even rows of another; on two copies of x the OR
+// of both is row 0 | row 1 in each half), a VALU op, where the ds_swizzle it replaces (lane ^ 16)
+// went through the LDS pipe that bounds the kernel.  Every lane of the wave must be active.
+#ifndef SDK_PROP32_PERMLANE
+#define SDK_PROP32_PERMLANE 1
+#endif
 __device__ __forceinline__ uint32_t p32_half_or(uint32_t x) {
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xF, 0xF, false);   // row_ror:1
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xF, 0xF, false);   // row_ror:2
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, false);   // row_ror:4
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);   // row_ror:8
+#if SDK_PROP32_PERMLANE
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return r[0] | r[1];
+#else
     x |= (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);
     return x;
+#endif
 }
 __device__ __forceinline__ uint32_t p32_half_and(uint32_t x) { return ~p32_half_or(~x); }
 

@@ -132,6 +132,21 @@ __device__ __forceinline__ uint2 p32_lda(uint32_t addr) {   // an absolute LDS a
     return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 }
 // stores volatile too: merged pairs become ds_write2_b64, 13 cycles against 2 x 6 (same table)
+// The unit phase's per-lane read-order table (p32_order_table): SDK_PROP32_TABLE16 keeps the nine
+// record addresses as 16-bit halves (three ds_read_b64 per step, halves split by VOP2 shifts and
+// masks) instead of 32-bit words (five reads) -- two LDS instructions fewer per step on the pipe
+// that bounds the kernel, for nine pairing VALU ops
+#ifndef SDK_PROP32_TABLE16
+#define SDK_PROP32_TABLE16 1
+#endif
+__device__ __forceinline__ uint64_t p32_tab64(const p32_lds_t* lds, uint32_t off) {
+    return *(const volatile __attribute__((address_space(3))) uint64_t*)(lds + off);
+}
+// 16-bit field k (0..3) of a table word
+__device__ __forceinline__ uint32_t p32_tab_field(uint64_t v, int k) {
+    const uint32_t w = k < 2 ? (uint32_t)v : (uint32_t)(v >> 32);
+    return (k & 1) ? w >> 16 : w & 0xFFFFu;
+}
 __device__ __forceinline__ void p32_st(p32_lds_t* base, uint32_t off, uint32_t x, uint32_t y) {
     *(volatile __attribute__((address_space(3))) uint64_t*)(base + off) = (uint64_t)x | ((uint64_t)y << 32);
 }
@@ -281,9 +296,17 @@ __device__ __forceinline__ uint32_t p32_dups(const P32Lane& w, const p32_lds_t* 
     // the unit's cells from p32_unit's order table (any order will do; no lane-dependent branch)
     const uint32_t tb = kP32Table + 40u * p32_opq(threadIdx.x);
     uint32_t T[9], dup = 0u;
+#if SDK_PROP32_TABLE16
+    uint64_t tw = 0ull;
+#endif
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
+#if SDK_PROP32_TABLE16
+        if (q % 4 == 0) tw = p32_tab64(lds, tb + 2u * q);
+        const uint32_t o = p32_tab_field(tw, q % 4);
+#else
         const uint32_t o = *(const volatile __attribute__((address_space(3))) uint32_t*)(lds + tb + 4u * (q < 3 ? q : q + 1));
+#endif
         const uint2 r0 = p32_lda(o), r1 = p32_lda(o + 8), r2 = p32_lda(o + 16), r3 = p32_lda(o + 24),
                     r4 = p32_lda(o + 32);
         const uint32_t a[9] = {r0.x, r0.y, r1.x, r1.y, r2.x, r2.y, r3.x, r3.y, r4.x};
@@ -313,19 +336,30 @@ __device__ __forceinline__ uint32_t p32_dups(const P32Lane& w, const p32_lds_t* 
 // so that those nine cells' records (40 B apart) fall in nine different bank pairs (cell index mod 32
 // distinct in every digit class; found by a search over relabelled and permuted pattern grids).  The
 // natural order met two addresses per bank pair on every read (15-16 % of the launch's LDS cycles
-// were bank conflicts).  The per-lane offsets are a table in LDS (12 words per lane, 3 reads a step).
+// were bank conflicts).  The per-lane offsets are a table in LDS (40 B per lane; SDK_PROP32_TABLE16 above).
 __device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds, uint32_t& miss) {
     const uint32_t j = p32_opq(w.hl);   // the unit record written below
     const uint32_t tb = kP32Table + 40u * p32_opq(threadIdx.x);
     uint32_t ones[9], twos[9], T[9];
+#if SDK_PROP32_TABLE16
+    uint64_t tA, tB = 0ull;   // table words: steps 0-3, 4-7 (step 8: its own read)
+#endif
     // cells 0, 1, 2
     {
         uint32_t a[3][9], s[3];
+#if SDK_PROP32_TABLE16
+        tA = p32_tab64(lds, tb);
+#else
         const uint64_t o01 = *(const volatile __attribute__((address_space(3))) uint64_t*)(lds + tb);
         const uint32_t o2 = *(const volatile __attribute__((address_space(3))) uint32_t*)(lds + tb + 8u);
+#endif
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
+#if SDK_PROP32_TABLE16
+            const uint32_t o = p32_tab_field(tA, q);
+#else
             const uint32_t o = q == 0 ? (uint32_t)o01 : q == 1 ? (uint32_t)(o01 >> 32) : o2;
+#endif
             const uint2 r0 = p32_lda(o), r1 = p32_lda(o + 8), r2 = p32_lda(o + 16), r3 = p32_lda(o + 24),
                         r4 = p32_lda(o + 32);
             a[q][0] = r0.x; a[q][1] = r0.y; a[q][2] = r1.x; a[q][3] = r1.y; a[q][4] = r2.x;
@@ -348,10 +382,30 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds,
                      "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]), "+v"(T[6]),
                      "+v"(T[7]), "+v"(T[8])::"memory");
         uint32_t a[2][9], s[2];
+#if SDK_PROP32_TABLE16
+        // steps 3 + 2p, 4 + 2p: (3, 4) from words A and B, (5, 6) from B, (7, 8) from B and C
+        uint32_t oo[2];
+        if (p == 0) {
+            tB = p32_tab64(lds, tb + 8u);
+            oo[0] = p32_tab_field(tA, 3);
+            oo[1] = p32_tab_field(tB, 0);
+        } else if (p == 1) {
+            oo[0] = p32_tab_field(tB, 1);
+            oo[1] = p32_tab_field(tB, 2);
+        } else {
+            oo[0] = p32_tab_field(tB, 3);
+            oo[1] = p32_tab_field(p32_tab64(lds, tb + 16u), 0);
+        }
+#else
         const uint64_t op = *(const volatile __attribute__((address_space(3))) uint64_t*)(lds + tb + 16u + 8u * p);
+#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+#if SDK_PROP32_TABLE16
+            const uint32_t o = oo[h];
+#else
             const uint32_t o = h == 0 ? (uint32_t)op : (uint32_t)(op >> 32);
+#endif
             const uint2 r0 = p32_lda(o), r1 = p32_lda(o + 8), r2 = p32_lda(o + 16), r3 = p32_lda(o + 24),
                         r4 = p32_lda(o + 32);
             a[h][0] = r0.x; a[h][1] = r0.y; a[h][2] = r1.x; a[h][3] = r1.y; a[h][4] = r2.x;
@@ -663,7 +717,12 @@ __device__ __forceinline__ void p32_order_table(p32_lds_t* lds) {
     for (uint32_t q = 0; q < 9; ++q) {
         const uint32_t o = u0 + (q % 3) * ua + (q / 3) * ub;
         const uint32_t t = kP32Order[o / kP32Rec];
+#if SDK_PROP32_TABLE16
+        static_assert(kP32Lds <= 65536u, "16-bit table entries");
+        ((__attribute__((address_space(3))) uint16_t*)tab)[t] = (uint16_t)(region + o);   // halves 0-8
+#else
         tab[t < 3u ? t : t + 1u] = region + o;   // words 0-2, then the pairs (3, 4) .. (7, 8) 8-byte aligned
+#endif
     }
 }
 

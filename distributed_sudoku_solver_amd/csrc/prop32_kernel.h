@@ -337,7 +337,12 @@ __device__ __forceinline__ uint32_t p32_dups(const P32Lane& w, const p32_lds_t* 
 // distinct in every digit class; found by a search over relabelled and permuted pattern grids).  The
 // natural order met two addresses per bank pair on every read (15-16 % of the launch's LDS cycles
 // were bank conflicts).  The per-lane offsets are a table in LDS (40 B per lane; SDK_PROP32_TABLE16 above).
-__device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds, uint32_t& miss) {
+// kDups (a group's first step): also the digits given twice in the unit (p32_dups) from the same
+// loaded records -- a digit closed in at least two of the unit's cells: the majority of three closed
+// terms over the first three cells, then of (closed so far, the pair's two closed terms) -- instead of
+// a second pass over the nine records
+template <bool kDups>
+__device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds, uint32_t& miss, uint32_t& dup) {
     const uint32_t j = p32_opq(w.hl);   // the unit record written below
     const uint32_t tb = kP32Table + 40u * p32_opq(threadIdx.x);
     uint32_t ones[9], twos[9], T[9];
@@ -368,6 +373,7 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds,
         }
 #pragma unroll
         for (int d = 0; d < 9; ++d) {
+            if (kDups) dup |= p32_b3<0xE8u>(a[0][d] & s[0], a[1][d] & s[1], a[2][d] & s[2]);
             p32_unit3(ones[d], twos[d], T[d], a[0][d], a[1][d], a[2][d], s[0], s[1], s[2]);
         }
     }
@@ -414,6 +420,7 @@ __device__ __forceinline__ void p32_unit(const P32Lane& w, const p32_lds_t* lds,
         }
 #pragma unroll
         for (int d = 0; d < 9; ++d) {
+            if (kDups) dup |= p32_b3<0xE8u>(T[d], a[0][d] & s[0], a[1][d] & s[1]);   // T: closed so far
             p32_unit2(ones[d], twos[d], T[d], a[0][d], a[1][d], s[0], s[1]);
         }
     }
@@ -838,15 +845,16 @@ __device__ __forceinline__ void prop32_body(Prop32Args a, uint64_t* stamps) {
                 __builtin_amdgcn_wave_barrier();
                 return;
             }
+            uint32_t miss, dup = 0u;
             if (it == 0) {   // a digit given twice: not exact, to the search
-                const uint32_t dup = p32_dups(w, lds);
+                p32_unit<true>(w, lds, miss, dup);
                 const uint64_t dupw = p32_mask64(p32_half_or(w.act ? dup : 0u)) & live;
                 undec |= dupw;
                 inexact |= dupw;
                 live &= ~dupw;
+            } else {
+                p32_unit<false>(w, lds, miss, dup);
             }
-            uint32_t miss;
-            p32_unit(w, lds, miss);
             const uint64_t badw = p32_mask64(p32_half_or(w.act ? (miss | empty) : 0u));
             const uint64_t allw = p32_mask64(p32_half_and(w.act ? alls : ~0u));
             const uint64_t sv = allw & ~badw & live, ct = badw & live;

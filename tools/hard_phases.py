@@ -6,7 +6,7 @@ prints each pass's wall time.  Under `rocprofv3 --kernel-trace` every dispatch o
 the trace: `tools/hard_phases_summary.py <dir>` splits it into passes and reports, per kernel, its
 span and the gaps between kernels (the GPU idle inside a pass).
 
-usage: python tools/hard_phases.py [--sets hard_1m,hard_100k] [--reps 5] [--order lex|mrv]
+usage: python tools/hard_phases.py [--sets hard_1m,hard_100k,heaviest_1000,minimal_1m] [--reps 5] [--order lex|mrv]
 """
 import argparse
 import json
@@ -42,6 +42,8 @@ def main():
                 p, s, _ = synth.load_hard(threads=16)
             elif name == "heaviest_1000":
                 p, s = synth.make_hard_heaviest(1000, threads=16)
+            elif name == "minimal_1m":    # the bench's minimal leg
+                p, s = synth.make_minimal_sym(1_048_576, base=65536, threads=16)
             else:
                 raise SystemExit(f"unknown set {name}")
             n = len(p)
